@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s of the MI355X ray march on BASELINE.json's headline
+config (C2: 256^3 synthetic grid, VCS + original, 1920x1080), plus the
+roofline of the dominant kernel and the CPU oracle baseline.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
+
+A step = one full frame: every rank renders its interleaved row bands
+(band b -> rank b % N; one rank = the whole frame), then (N > 1) the bands are
+gathered to rank 0 over RCCL and reassembled.  The frame is fixed while N
+grows ("scaling": "strong").  Inputs (scene, camera) are resident in HBM
+before timing starts.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import voxelraymarcher_amd as vr  # noqa: E402
+from voxelraymarcher_amd.tiles import assemble_bands  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+BAND_ROWS = 8              # one wave tile high
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="C2", choices=sorted(vr.CONFIGS))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (default min(16, cpus))")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="PMC-derived HBM bytes per launch (written by profiles/collect_traffic.py)")
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, xyz, rgb, threads: int) -> dict:
+    """Oracle (clean-room C restatement, OpenMP) on the host cores: the whole
+    frame of the same workload, timed once after a small warm-up."""
+    import oracle
+    scene = oracle.Scene(xyz, rgb, int(cfg.store))
+    cam = oracle.reference_camera(cfg.width, cfg.height)
+    lit = oracle.lighting()
+    scene.render(int(cfg.algorithm), cam, lit, cfg.width, cfg.height, cfg.scale, row_begin=0, row_end=8,
+                 nthreads=threads)
+    t0 = time.perf_counter()
+    scene.render(int(cfg.algorithm), cam, lit, cfg.width, cfg.height, cfg.scale, nthreads=threads)
+    dt = time.perf_counter() - t0
+    rays = cfg.width * cfg.height
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"full {cfg.width}x{cfg.height} frame of {cfg.name} ({rays} primary rays), "
+                      f"oracle/vr_oracle.c -O2 OpenMP {threads} threads, {dt:.2f} s wall"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = vr.CONFIGS[args.config]
+    xyz, rgb = cfg.voxels()
+    scene = vr.create_scene(xyz, rgb, cfg.store, device=local)
+    W, H = cfg.width, cfg.height
+    cam = vr.Camera.reference(W, H)
+    lit = vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    words = vr.band_buffer_words(W, H, BAND_ROWS, world)
+    buf = torch.empty(words, dtype=torch.int32, device=dev)
+    gathered = [torch.empty_like(buf) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream()
+
+    def render():
+        vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, rank, world, buf, stream)
+
+    def step():
+        render()
+        if world > 1:
+            dist.gather(buf, gathered, dst=0)
+            if rank == 0:
+                assemble_bands(torch.stack(gathered), W, H, BAND_ROWS)
+
+    # algorithmic bytes of one launch (instrumented kernel, untimed)
+    ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    full = torch.empty(W * H, dtype=torch.int32, device=dev)
+    vr.render_count(scene, cfg.algorithm, cam, lit, info, W, H, full, ctr)
+    torch.cuda.synchronize()
+    frame_bytes = int(ctr.item())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # kernel-only timing on the launch stream (HIP events), untimed region for the step clock
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a, b in ev:
+        a.record(stream)
+        render()
+        b.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ms_per_step = dt / args.steps * 1e3
+    mrays = W * H / (ms_per_step * 1e-3) / 1e6
+
+    if rank == 0:
+        # bytes of this rank's launch ~ frame bytes / world (bands interleave finely)
+        launch_bytes = frame_bytes / world
+        achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("config") == cfg.name and tj.get("world") == world:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        line = {
+            "metric": "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s",
+            "value": round(mrays, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (counter-hash voxel grid, SURVEY.md 8(d))",
+            "config": {"workload": f"{cfg.name}: {cfg.notes}", "grid": cfg.grid, "width": W, "height": H,
+                       "store": cfg.store.name, "algorithm": cfg.algorithm.name, "scale": cfg.scale,
+                       "voxels": int(len(rgb)), "parallelism": f"row-band tiles x{world}" +
+                       (" + RCCL gather" if world > 1 else "")},
+            "kernel_ms": round(kern_ms, 4),
+            "kernel_mrays_per_s": round(W * H / world / (kern_ms * 1e-3) / 1e6, 2),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": int(launch_bytes)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(cfg, xyz, rgb, threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+/*
+ * vr.h -- C ABI of the MI355X-native voxel ray-march renderer (libvr.so).
+ *
+ * Drop-in boundary for the hot path of lukeduball/VoxelRaymarcher.  Every
+ * entry point names the reference interface it replaces (paths relative to
+ * /root/reference/VoxelRaymarcher/src).  No HIP or torch types appear in the
+ * signatures: device buffers are plain pointers, streams are `void*`
+ * (a hipStream_t, NULL = the null stream).
+ *
+ * Return codes: VR_OK (0) or a negative VR_E_*; vr_last_error() gives a
+ * thread-local message for the last failure on the calling thread.
+ */
+#ifndef VR_H
+#define VR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VR_OK 0
+#define VR_E_INVALID (-1)   /* bad argument */
+#define VR_E_HIP (-2)       /* HIP runtime error / no device */
+#define VR_E_NOMEM (-3)     /* host or device allocation failed */
+#define VR_E_IO (-4)        /* file could not be read or written */
+#define VR_E_BUILD (-5)     /* storage structure could not be built */
+#define VR_E_PARSE (-6)     /* malformed .vox line (std::stoi would throw) */
+
+/* = enum class StorageType {VOXEL_CLUSTER_STORE, HASH_TABLE}
+ *   (geometry/VoxelFunctions.cuh:37; selected in main/Main.cu:45-55) */
+typedef enum { VR_STORE_VCS = 0, VR_STORE_HASHTABLE = 1 } vr_store;
+
+/* = rayMarchFunctionID (main/Main.cu:58-68,119-128):
+ *   0 -> rayMarchSceneJumpAxis, 1 -> rayMarchSceneOriginal */
+typedef enum { VR_ALGO_LONGESTAXIS = 0, VR_ALGO_ORIGINAL = 1 } vr_algo;
+
+/* = class Camera field order (renderer/camera/Camera.cuh:34-39) */
+typedef struct {
+    float origin[3];
+    float lower_left[3];
+    float horizontal[3];
+    float vertical[3];
+    float forward[3];
+} vr_camera;
+
+/* = the __constant__ block LIGHT_DIRECTION / LIGHT_COLOR / LIGHT_POSITION /
+ *   USE_POINT_LIGHT / USE_SHADOWS (geometry/VoxelFunctions.cuh:27-35) as
+ *   uploaded by setupConstantValues (main/Main.cu:26-42). */
+typedef struct {
+    float light_dir[3];
+    float light_color[3];
+    float light_pos[3];
+    int32_t use_point_light;
+    int32_t use_shadows;
+} vr_lighting;
+
+/* Immutable per-device scene: region table + VCS or cuckoo storage images.
+ * Replaces VoxelSceneCPU::generateVoxelScene's device pointer table
+ * (geometry/VoxelSceneCPU.cuh:49-93) plus the device-side virtual adapters
+ * built by the generateVoxelScene kernel (renderer/Renderer.cuh:1066-1086). */
+typedef struct vr_scene vr_scene;
+
+typedef struct {
+    uint32_t diameter;       /* = VoxelSceneCPU::getArrayDiameter (VoxelSceneCPU.cuh:107-110) */
+    int32_t min_coord;       /* = VoxelSceneCPU::getMinCoord (:118-121) */
+    uint32_t region_count;   /* non-empty 64^3 regions */
+    uint32_t store;          /* vr_store */
+    uint64_t voxel_count;    /* distinct voxels after duplicate resolution */
+    uint64_t device_bytes;   /* HBM footprint of the scene */
+    int32_t device;
+} vr_scene_info;
+
+/* Synthetic grid generator; counter-hash occupancy. */
+typedef struct {
+    uint32_t n;              /* grid side, multiple of 64, <= 1024 */
+    double p_region, p_cluster, p_voxel;
+    uint64_t seed;
+} vr_synth_params;
+
+/* Camera::Camera(o, lookAt, globalUp, fov, aspect) (Camera.cuh:11-23), host. */
+int vr_camera_make(const float eye[3], const float look_at[3], const float up[3],
+                   float fov_deg, float aspect, vr_camera* out);
+
+/* setupConstantValues defaults (Main.cu:26-42): directional light
+ * normalize(1,1,1), white, point light at (10,10,-10) disabled, shadows on. */
+int vr_lighting_default(vr_lighting* out);
+
+/* VoxelSceneCPU::insertVoxel for every voxel (VoxelSceneCPU.cuh:16-46), then
+ * generateVoxelScene(storageType) (:49-93) -- VoxelClusterStore ctor
+ * (storage/VoxelClusterStore.cuh:37-85) or CuckooHashTable ctor
+ * (storage/CuckooHashTable.cuh:20-49,97-178) per region -- and the upload to
+ * `device`.  xyz: 3n int32 world voxel coordinates; rgb: n colours
+ * 0x00RRGGBB (must be < 2^24).  Later duplicates overwrite earlier ones. */
+int vr_scene_create(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb,
+                    size_t n, vr_scene** out);
+
+/* VoxelFile::readVoxelFile (geometry/VoxelFile.cuh:9-35) + vr_scene_create.
+ * Unlike the reference the path is used as given (no "resources/" prefix). */
+int vr_scene_load_vox(int device, vr_store store, const char* path, vr_scene** out);
+
+int vr_scene_get_info(const vr_scene* s, vr_scene_info* out);
+void vr_scene_destroy(vr_scene* s);
+
+/* rayMarchSceneOriginal / rayMarchSceneJumpAxis (Renderer.cuh:1033-1063) as
+ * launched by runRaymarchingKernel (Main.cu:105-163), for image rows
+ * [row_begin, row_end) of a width x height frame.  out_dev: device buffer of
+ * (row_end-row_begin)*width uint32, row-major, y = 0 the top row, each the
+ * packed 0x00RRGGBB word the reference hands to writeColorToFramebuffer
+ * (Renderer.cuh:1024-1031).  translation/scale = VoxelSceneInfo
+ * (renderer/VoxelSceneInfo.cuh:5-15).  Asynchronous on `stream`. */
+int vr_render(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
+              const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
+              uint32_t row_begin, uint32_t row_end, uint32_t* out_dev, void* stream);
+
+/* Multi-GPU tile partition: the frame is cut into bands of band_rows rows;
+ * band b belongs to rank b % nranks.  out_dev holds this rank's bands packed
+ * in order: ceil(ceil(height/band_rows)/nranks)*band_rows*width uint32
+ * (rows past the frame or past this rank's last band are written as 0), so
+ * every rank's buffer has the same size for an RCCL gather. */
+int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
+                    const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
+                    uint32_t band_rows, uint32_t rank, uint32_t nranks, uint32_t* out_dev,
+                    void* stream);
+/* Number of uint32 words vr_render_bands writes per rank. */
+uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t nranks);
+
+/* Same render as vr_render, plus the SURVEY.md 8(d) algorithmic byte count of
+ * the launch accumulated into *bytes_dev (device uint64, caller-zeroed).
+ * Instrumented variant for measurement; pixels are identical. */
+int vr_render_count(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
+                    const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
+                    uint32_t row_begin, uint32_t row_end, uint32_t* out_dev,
+                    uint64_t* bytes_dev, void* stream);
+
+/* writeColorToFramebuffer (Renderer.cuh:1024-1031): packed words -> RGB8
+ * (3 bytes per pixel, R = word >> 16 truncated to 8 bits), on the device. */
+int vr_pack_rgb8(const uint32_t* words_dev, uint8_t* rgb_dev, uint64_t n_pixels, void* stream);
+
+/* Synthetic scene: with xyz == NULL only counts (*n_out); otherwise writes up
+ * to `capacity` voxels (3 int32 + 1 colour each) and sets *n_out. */
+int vr_synth_generate(const vr_synth_params* p, int32_t* xyz, uint32_t* rgb, size_t capacity,
+                      size_t* n_out);
+
+/* .vox CSV reader/writer ("x,y,z,color" per line, VoxelFile.cuh:11-35).
+ * Reader: two-phase like vr_synth_generate. */
+int vr_vox_read(const char* path, int32_t* xyz, uint32_t* rgb, size_t capacity, size_t* n_out);
+int vr_vox_write(const char* path, const int32_t* xyz, const uint32_t* rgb, size_t n);
+
+const char* vr_last_error(void);
+const char* vr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VR_H */

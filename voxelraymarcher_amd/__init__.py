@@ -1,0 +1,19 @@
+"""voxelraymarcher_amd -- MI355X-native voxel ray-march renderer.
+
+Drop-in for the hot path of lukeduball/VoxelRaymarcher: the per-pixel ray
+march (original 3-axis DDA and longest-axis jump) over the VoxelClusterStore
+and CuckooHashTable lookups, as hand-written HIP for gfx950 behind the C ABI
+in include/vr.h (libvr.so).  This package is the Python host mirror used by
+the tests and the benchmark; the C++ host mirror is include/vr.hpp and the
+CLI is bin/VoxelRaymarcher.
+"""
+from ._capi import LIB_PATH, VrError, lib
+from .renderer import (CONFIGS, Camera, DeviceScene, RayMarchAlgorithm, RenderConfig, StorageType, VoxelSceneCPU,
+                       VoxelSceneInfo, band_buffer_words, create_scene, pack_rgb8, parse_algorithm, parse_storage,
+                       read_voxel_file, render_bands, render_count, run_raymarching_kernel, setup_constant_values,
+                       synth_scene, write_voxel_file)
+
+__all__ = ["LIB_PATH", "VrError", "lib", "CONFIGS", "Camera", "DeviceScene", "RayMarchAlgorithm", "RenderConfig",
+           "StorageType", "VoxelSceneCPU", "VoxelSceneInfo", "band_buffer_words", "create_scene", "pack_rgb8",
+           "parse_algorithm", "parse_storage", "read_voxel_file", "render_bands", "render_count",
+           "run_raymarching_kernel", "setup_constant_values", "synth_scene", "write_voxel_file"]

@@ -1,0 +1,621 @@
+// vr_host.cpp -- host side of libvr.so: scene build (region bucketing, VCS
+// and cuckoo images), device upload, the C ABI of include/vr.h, the
+// synthetic grid generator and the .vox CSV reader/writer.
+//
+// Replaces, on the host: VoxelSceneCPU (geometry/VoxelSceneCPU.cuh:13-131),
+// the VoxelClusterStore / CuckooHashTable constructors
+// (storage/VoxelClusterStore.cuh:37-85, storage/CuckooHashTable.cuh:20-178),
+// VoxelFile::readVoxelFile (geometry/VoxelFile.cuh:9-35), Camera::Camera
+// (renderer/camera/Camera.cuh:11-23) and runRaymarchingKernel
+// (main/Main.cu:105-163).  The nested unordered_maps of the reference become
+// one sort of (region, key) records; pointers become 32-bit offsets.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vr.h"
+#include "vr_internal.h"
+
+namespace {
+
+thread_local std::string g_err = "";
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+    return fail(VR_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// static_cast<int32_t>(float) with the CUDA semantics used on the device.
+inline int32_t f2i(float f) {
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return INT32_MAX;
+    if (f <= -2147483648.0f) return INT32_MIN;
+    return (int32_t)f;
+}
+
+// ---------------------------------------------------------------- camera math
+struct f3 { float x, y, z; };
+inline f3 add(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline f3 sub(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline f3 scl(float t, f3 a) { return {t * a.x, t * a.y, t * a.z}; }
+inline f3 unit(f3 a) {
+    float len = std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+    return {a.x / len, a.y / len, a.z / len};
+}
+inline f3 cross(f3 a, f3 b) {   // Vector3.cuh:154-159
+    return {(a.y * b.z - a.z * b.y), (-(a.x * b.z - a.z * b.x)), (a.x * b.y - a.y * b.x)};
+}
+
+// ------------------------------------------------------------- cuckoo hashing
+const uint32_t kPrimes[14] = {668265261u, 12289u, 24593u, 49157u, 98317u, 196613u, 393241u,
+                              786433u, 1572869u, 3145739u, 6291469u, 12582917u, 25165843u, 50331653u};
+
+inline uint32_t hash1(uint32_t k, uint32_t offset) {   // CuckooHashTable.cuh:181-190
+    k = (k + 0x7ed55d16u) + (k << 12);
+    k = (k ^ 0xc761c23cu) ^ (uint32_t)((int32_t)k >> 19);
+    k = (k + 0x165667b1u) + (k << 5);
+    k = (k + 0xd3a2646cu) ^ (k << 9);
+    k = (k + 0xfd7046c5u) + (k << 3);
+    k = (k ^ 0xb55a4f09u) ^ (uint32_t)((int32_t)k >> 16);
+    return k + offset;
+}
+inline uint32_t hash2(uint32_t k, uint32_t prime) {    // CuckooHashTable.cuh:193-202
+    k = (k ^ 61u) ^ (uint32_t)((int32_t)k >> 16);
+    k = k + (k << 3);
+    k = k ^ (uint32_t)((int32_t)k >> 4);
+    k = k * prime;
+    k = k ^ (uint32_t)((int32_t)k >> 15);
+    return k;
+}
+
+// createCuckooHashTable (CuckooHashTable.cuh:97-178) into interleaved
+// {key,value} slots: table 1 at slots[0..M), table 2 at slots[M..2M).
+// The rehash draws a new prime/offset from a seeded generator instead of
+// rand() (Random.cuh:14-18): lookups do not depend on the placement.
+bool cuckoo_build(const uint32_t* keys, const uint32_t* vals, uint32_t n, uint32_t* M_out,
+                  uint32_t* prime_out, uint32_t* offset_out, std::vector<uint32_t>& slots,
+                  size_t base_words) {
+    const uint32_t M = (uint32_t)((double)n * 1.25);   // numElements * 1.25 (:23)
+    uint32_t prime = kPrimes[0], offset = 0;
+    uint64_t rng = 0x9E3779B97F4A7C15ull ^ (uint64_t)n ^ ((uint64_t)keys[0] << 20);
+    uint32_t* t = nullptr;
+    for (int attempt = 0; attempt < 4096; ++attempt) {
+        slots.resize(base_words + 4 * (size_t)M);
+        t = slots.data() + base_words;
+        for (uint32_t i = 0; i < 2 * M; ++i) { t[2 * i] = vr::kEmpty; t[2 * i + 1] = 0; }
+        bool rehash = false;
+        for (uint32_t i = 0; i < n && !rehash; ++i) {
+            uint32_t code = keys[i], value = vals[i], bucket = 0, it = 0;
+            for (;;) {
+                if (it >= 300000u) { rehash = true; break; }
+                uint32_t* slot = bucket == 0 ? t + 2 * (size_t)(hash1(code, offset) % M)
+                                             : t + 2 * ((size_t)M + hash2(code, prime) % M);
+                if (slot[0] == vr::kEmpty) { slot[0] = code; slot[1] = value; break; }
+                std::swap(slot[0], code);
+                std::swap(slot[1], value);
+                bucket ^= 1u;
+                ++it;
+            }
+        }
+        if (!rehash) {
+            *M_out = M; *prime_out = prime; *offset_out = offset;
+            return true;
+        }
+        rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+        prime = kPrimes[(rng >> 33) % 14u];
+        rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+        offset = (uint32_t)((rng >> 33) % 25u);
+    }
+    return false;
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct vr_scene {
+    int device = 0;
+    vr_store store = VR_STORE_VCS;
+    uint32_t D = 1;
+    int32_t min_coord = 0;
+    uint32_t n_regions = 0;
+    uint64_t n_voxels = 0;
+    DevBuf region_slot, vcs_dir, vcs_pool, ht_meta, ht_slots;
+    uint64_t device_bytes() const {
+        return region_slot.bytes + vcs_dir.bytes + vcs_pool.bytes + ht_meta.bytes + ht_slots.bytes;
+    }
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+void free_scene(vr_scene* s) {
+    if (!s) return;
+    DevBuf* bufs[] = {&s->region_slot, &s->vcs_dir, &s->vcs_pool, &s->ht_meta, &s->ht_slots};
+    for (DevBuf* b : bufs)
+        if (b->p) (void)hipFree(b->p);
+    delete s;
+}
+
+int upload(DevBuf& b, const void* src, size_t bytes) {
+    b.bytes = bytes;
+    if (bytes == 0) return VR_OK;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) return fail(VR_E_NOMEM, std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    e = hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy H2D");
+    return VR_OK;
+}
+
+// One record per inserted voxel: (region index, local key) sort key.
+struct Rec {
+    uint64_t k;       // region << 32 | key
+    uint32_t val;
+    uint32_t idx;     // insertion order (later wins)
+};
+
+int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, vr_scene** out) {
+    if (!out) return fail(VR_E_INVALID, "out is NULL");
+    *out = nullptr;
+    if (store != VR_STORE_VCS && store != VR_STORE_HASHTABLE) return fail(VR_E_INVALID, "unknown store");
+    if (n && (!xyz || !rgb)) return fail(VR_E_INVALID, "xyz/rgb NULL");
+    if (n >= 0xFFFFFFFFull) return fail(VR_E_INVALID, "too many voxels");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(VR_E_HIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(VR_E_INVALID, "device index out of range");
+
+    // VoxelSceneCPU::insertVoxel (VoxelSceneCPU.cuh:16-46)
+    std::vector<int32_t> rc(3 * n);
+    int32_t minc = 0, maxc = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (rgb[i] > 0xFFFFFFu)
+            return fail(VR_E_INVALID, "voxel colour " + std::to_string(rgb[i]) + " at index " + std::to_string(i) +
+                                          " exceeds 24-bit RGB");
+        for (int a = 0; a < 3; ++a) {
+            int32_t c = f2i(std::floor((float)xyz[3 * i + a] / 64.0f));   // :19-21
+            rc[3 * i + a] = c;
+            minc = std::min(minc, c);
+            maxc = std::max(maxc, c);
+        }
+    }
+    const int64_t D64 = (int64_t)maxc - (int64_t)minc + 1;
+    if (D64 > 1024) return fail(VR_E_INVALID, "scene spans more than 1024 regions per axis");
+    const uint32_t D = (uint32_t)D64;
+    const uint64_t D3 = (uint64_t)D * D * D;
+
+    std::vector<Rec> recs(n);
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t l[3];
+        for (int a = 0; a < 3; ++a) {
+            int32_t c = xyz[3 * i + a];
+            l[a] = (uint32_t)(((c % vr::kBlock) + vr::kBlock) % vr::kBlock);    // :24-26
+        }
+        uint64_t ax = (uint64_t)(rc[3 * i] - minc), ay = (uint64_t)(rc[3 * i + 1] - minc),
+                 az = (uint64_t)(rc[3 * i + 2] - minc);
+        uint64_t region = ax + ay * D + az * (uint64_t)D * D;
+        uint32_t key = (l[0] << 20) | (l[1] << 10) | l[2];                     // generate3DPoint
+        recs[i] = Rec{(region << 32) | key, rgb[i], (uint32_t)i};
+    }
+    std::vector<int32_t>().swap(rc);
+    std::sort(recs.begin(), recs.end(), [](const Rec& a, const Rec& b) { return a.k < b.k || (a.k == b.k && a.idx < b.idx); });
+    size_t m = 0;   // duplicates: the later insertion wins (map assignment, :46)
+    for (size_t i = 0; i < n; ++i) {
+        if (m && recs[m - 1].k == recs[i].k) recs[m - 1] = recs[i];
+        else recs[m++] = recs[i];
+    }
+    recs.resize(m);
+
+    std::vector<uint32_t> region_slot(D3, vr::kNone);
+    std::vector<size_t> region_begin;
+    for (size_t i = 0; i < m; ++i)
+        if (i == 0 || (recs[i].k >> 32) != (recs[i - 1].k >> 32)) {
+            region_slot[recs[i].k >> 32] = (uint32_t)region_begin.size();
+            region_begin.push_back(i);
+        }
+    const uint32_t nr = (uint32_t)region_begin.size();
+    region_begin.push_back(m);
+
+    vr_scene* s = new vr_scene();
+    s->device = device; s->store = store; s->D = D; s->min_coord = minc; s->n_regions = nr; s->n_voxels = m;
+    DeviceGuard dg(device);
+    int rc_up = upload(s->region_slot, region_slot.data(), region_slot.size() * 4);
+    if (rc_up) { free_scene(s); return rc_up; }
+
+    if (store == VR_STORE_VCS) {
+        // VoxelClusterStore ctor (VoxelClusterStore.cuh:37-85), SoA blocks.
+        std::vector<uint32_t> dir((size_t)nr * 512, vr::kNone);
+        std::vector<uint32_t> pool;
+        pool.reserve(2 * m + 16);
+        std::vector<uint32_t> cid_of;
+        for (uint32_t r = 0; r < nr; ++r) {
+            size_t b = region_begin[r], e = region_begin[r + 1];
+            uint32_t counts[512] = {0};
+            cid_of.resize(e - b);
+            for (size_t i = b; i < e; ++i) {
+                uint32_t key = (uint32_t)recs[i].k;
+                uint32_t x = key >> 20, y = (key >> 10) & 0x3FFu, z = key & 0x3FFu;
+                uint32_t c = ((x / 8u) << 6) | ((y / 8u) << 3) | (z / 8u);
+                cid_of[i - b] = c;
+                counts[c]++;
+            }
+            uint32_t pos[512];
+            for (uint32_t c = 0; c < 512; ++c) {
+                if (!counts[c]) continue;
+                if (pool.size() + 1 + 2 * (size_t)counts[c] >= 0xFFFFFFFFull) { free_scene(s); return fail(VR_E_BUILD, "VCS pool exceeds 32-bit offsets"); }
+                dir[(size_t)r * 512 + c] = (uint32_t)pool.size();
+                pool.push_back(counts[c]);
+                pos[c] = (uint32_t)pool.size();
+                pool.resize(pool.size() + 2 * (size_t)counts[c]);
+            }
+            uint32_t fill[512] = {0};
+            for (size_t i = b; i < e; ++i) {        // keys arrive ascending: blocks stay sorted
+                uint32_t c = cid_of[i - b];
+                pool[pos[c] + fill[c]] = (uint32_t)recs[i].k;
+                pool[pos[c] + counts[c] + fill[c]] = recs[i].val;
+                fill[c]++;
+            }
+        }
+        if (pool.empty()) pool.push_back(0);
+        if ((rc_up = upload(s->vcs_dir, dir.data(), dir.size() * 4)) ||
+            (rc_up = upload(s->vcs_pool, pool.data(), pool.size() * 4))) {
+            free_scene(s);
+            return rc_up;
+        }
+    } else {
+        // CuckooHashTable ctor (CuckooHashTable.cuh:20-49) per region.
+        std::vector<uint32_t> meta((size_t)nr * 4);
+        std::vector<uint32_t> slots;
+        std::vector<uint32_t> keys, vals;
+        for (uint32_t r = 0; r < nr; ++r) {
+            size_t b = region_begin[r], e = region_begin[r + 1];
+            keys.resize(e - b); vals.resize(e - b);
+            for (size_t i = b; i < e; ++i) { keys[i - b] = (uint32_t)recs[i].k; vals[i - b] = recs[i].val; }
+            size_t base_words = slots.size();
+            uint32_t M = 0, prime = 0, offset = 0;
+            if (!cuckoo_build(keys.data(), vals.data(), (uint32_t)(e - b), &M, &prime, &offset, slots, base_words)) {
+                free_scene(s);
+                return fail(VR_E_BUILD, "cuckoo hash table build failed for region " + std::to_string(r));
+            }
+            if (base_words / 2 >= 0xFFFFFFFFull) { free_scene(s); return fail(VR_E_BUILD, "hash slots exceed 32-bit offsets"); }
+            meta[4 * r + 0] = (uint32_t)(base_words / 2);
+            meta[4 * r + 1] = M;
+            meta[4 * r + 2] = prime;
+            meta[4 * r + 3] = offset;
+        }
+        if (slots.empty()) slots.assign(2, vr::kEmpty);
+        if (meta.empty()) meta.assign(4, 0);
+        if ((rc_up = upload(s->ht_meta, meta.data(), meta.size() * 4)) ||
+            (rc_up = upload(s->ht_slots, slots.data(), slots.size() * 4))) {
+            free_scene(s);
+            return rc_up;
+        }
+    }
+    *out = s;
+    return VR_OK;
+}
+
+vr::KScene kscene(const vr_scene* s) {
+    vr::KScene k{};
+    k.region_slot = (const uint32_t*)s->region_slot.p;
+    k.vcs_dir = (const uint32_t*)s->vcs_dir.p;
+    k.vcs_pool = (const uint32_t*)s->vcs_pool.p;
+    k.ht_meta = (const uint4*)s->ht_meta.p;
+    k.ht_slots = (const uint2*)s->ht_slots.p;
+    k.D = s->D;
+    k.min_coord = s->min_coord;
+    return k;
+}
+
+int make_view(const vr_scene* s, const vr_camera* cam, const vr_lighting* lit, const float translation[3],
+              uint32_t scale, uint32_t width, uint32_t height, vr::KView& v) {
+    if (!s) return fail(VR_E_INVALID, "scene is NULL");
+    if (!cam || !lit) return fail(VR_E_INVALID, "camera/lighting NULL");
+    if (width == 0 || height == 0 || width > 65536 || height > 65536) return fail(VR_E_INVALID, "bad image size");
+    memset(&v, 0, sizeof v);
+    for (int i = 0; i < 3; ++i) {
+        v.llc[i] = cam->lower_left[i]; v.hor[i] = cam->horizontal[i]; v.ver[i] = cam->vertical[i];
+        v.org[i] = cam->origin[i];
+        v.L[i] = lit->light_dir[i]; v.LC[i] = lit->light_color[i]; v.LP[i] = lit->light_pos[i];
+        v.translation[i] = translation ? translation[i] : 0.0f;
+    }
+    v.scale_f = (float)scale;          // static_cast<float>(scale) (Ray.cuh:16)
+    v.use_point_light = lit->use_point_light ? 1 : 0;
+    v.use_shadows = lit->use_shadows ? 1 : 0;
+    v.W = width;
+    v.H = height;
+    return VR_OK;
+}
+
+int launch(const vr_scene* s, vr_algo algo, bool count, vr::KView& v, void* stream) {
+    if (algo != VR_ALGO_ORIGINAL && algo != VR_ALGO_LONGESTAXIS) return fail(VR_E_INVALID, "unknown algorithm");
+    DeviceGuard dg(s->device);
+    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "ray-march launch");
+    return VR_OK;
+}
+
+// ------------------------------------------------------------- synthetic grid
+inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+inline bool draw(uint64_t seed, uint64_t stream, uint64_t k, double p) {
+    uint64_t h = splitmix64((seed << 34) | (stream << 32) | k);
+    return (double)(h >> 40) * (1.0 / 16777216.0) < p;
+}
+
+// std::stoi as used by VoxelFile.cuh:18-21: skip leading whitespace, optional
+// sign, at least one digit, stop at the first non-digit; out of int range or
+// no digits throws in the reference -> VR_E_PARSE here.
+bool stoi_like(const char* b, const char* e, int32_t* out) {
+    while (b < e && (*b == ' ' || *b == '\t' || *b == '\n' || *b == '\v' || *b == '\f' || *b == '\r')) ++b;
+    bool neg = false;
+    if (b < e && (*b == '+' || *b == '-')) { neg = *b == '-'; ++b; }
+    if (b >= e || *b < '0' || *b > '9') return false;
+    int64_t v = 0;
+    while (b < e && *b >= '0' && *b <= '9') {
+        v = v * 10 + (*b - '0');
+        if (v > 2147483648ll) return false;
+        ++b;
+    }
+    if (neg) v = -v;
+    if (v > 2147483647ll || v < -2147483648ll) return false;
+    *out = (int32_t)v;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* vr_last_error(void) { return g_err.c_str(); }
+const char* vr_version(void) { return "voxelraymarcher_amd 0.1 (gfx950)"; }
+
+int vr_camera_make(const float eye[3], const float look_at[3], const float up[3], float fov_deg, float aspect,
+                   vr_camera* out) {
+    if (!eye || !look_at || !up || !out) return fail(VR_E_INVALID, "NULL argument");
+    const float PI = 3.141592f;                                 // MathConstants.cuh:3
+    float half_h = std::tan((fov_deg * PI / 180.f) / 2.0f);     // Camera.cuh:13
+    float half_w = half_h * aspect;
+    f3 o{eye[0], eye[1], eye[2]};
+    f3 w = unit(sub(f3{look_at[0], look_at[1], look_at[2]}, o));
+    f3 u = unit(cross(w, f3{up[0], up[1], up[2]}));
+    f3 v = cross(u, w);
+    f3 llc = add(sub(sub(o, scl(half_w, u)), scl(half_h, v)), w);   // :19
+    f3 hor = scl(2 * half_w, u), ver = scl(2 * half_h, v);
+    const f3* src[5] = {&o, &llc, &hor, &ver, &w};
+    float* dst[5] = {out->origin, out->lower_left, out->horizontal, out->vertical, out->forward};
+    for (int i = 0; i < 5; ++i) { dst[i][0] = src[i]->x; dst[i][1] = src[i]->y; dst[i][2] = src[i]->z; }
+    return VR_OK;
+}
+
+int vr_lighting_default(vr_lighting* out) {
+    if (!out) return fail(VR_E_INVALID, "NULL argument");
+    f3 L = unit(f3{1.0f, 1.0f, 1.0f});                          // Main.cu:28
+    out->light_dir[0] = L.x; out->light_dir[1] = L.y; out->light_dir[2] = L.z;
+    for (int i = 0; i < 3; ++i) out->light_color[i] = 1.0f;    // :31
+    out->light_pos[0] = 10.0f; out->light_pos[1] = 10.0f; out->light_pos[2] = -10.0f;   // :34
+    out->use_point_light = 0;                                   // :37
+    out->use_shadows = 1;                                       // :40
+    return VR_OK;
+}
+
+int vr_scene_create(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, vr_scene** out) {
+    return build_scene(device, store, xyz, rgb, n, out);
+}
+
+int vr_scene_load_vox(int device, vr_store store, const char* path, vr_scene** out) {
+    size_t n = 0;
+    int rc = vr_vox_read(path, nullptr, nullptr, 0, &n);
+    if (rc) return rc;
+    std::vector<int32_t> xyz(3 * n + 3);
+    std::vector<uint32_t> rgb(n + 1);
+    rc = vr_vox_read(path, xyz.data(), rgb.data(), n, &n);
+    if (rc) return rc;
+    return build_scene(device, store, xyz.data(), rgb.data(), n, out);
+}
+
+int vr_scene_get_info(const vr_scene* s, vr_scene_info* out) {
+    if (!s || !out) return fail(VR_E_INVALID, "NULL argument");
+    out->diameter = s->D;
+    out->min_coord = s->min_coord;
+    out->region_count = s->n_regions;
+    out->store = (uint32_t)s->store;
+    out->voxel_count = s->n_voxels;
+    out->device_bytes = s->device_bytes();
+    out->device = s->device;
+    return VR_OK;
+}
+
+void vr_scene_destroy(vr_scene* s) {
+    if (!s) return;
+    DeviceGuard dg(s->device);
+    free_scene(s);
+}
+
+int vr_render(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit, const float translation[3],
+              uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin, uint32_t row_end, uint32_t* out_dev,
+              void* stream) {
+    vr::KView v;
+    int rc = make_view(s, cam, lit, translation, scale, width, height, v);
+    if (rc) return rc;
+    if (row_begin > row_end || row_end > height) return fail(VR_E_INVALID, "bad row range");
+    if (!out_dev) return fail(VR_E_INVALID, "out_dev is NULL");
+    v.row0 = row_begin;
+    v.band_rows = std::max(1u, row_end - row_begin);
+    v.rank = 0; v.nranks = 1;
+    v.local_rows = row_end - row_begin;
+    v.out = out_dev;
+    return launch(s, algo, false, v, stream);
+}
+
+uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t nranks) {
+    if (!band_rows || !nranks) return 0;
+    uint64_t nb = (height + (uint64_t)band_rows - 1) / band_rows;
+    uint64_t per = (nb + nranks - 1) / nranks;
+    return per * band_rows * (uint64_t)width;
+}
+
+int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
+                    const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t band_rows,
+                    uint32_t rank, uint32_t nranks, uint32_t* out_dev, void* stream) {
+    vr::KView v;
+    int rc = make_view(s, cam, lit, translation, scale, width, height, v);
+    if (rc) return rc;
+    if (!band_rows || !nranks || rank >= nranks) return fail(VR_E_INVALID, "bad band partition");
+    if (!out_dev) return fail(VR_E_INVALID, "out_dev is NULL");
+    uint64_t words = vr_band_buffer_words(width, height, band_rows, nranks);
+    v.row0 = 0;
+    v.band_rows = band_rows;
+    v.rank = rank;
+    v.nranks = nranks;
+    v.local_rows = (uint32_t)(words / width);
+    v.out = out_dev;
+    return launch(s, algo, false, v, stream);
+}
+
+int vr_render_count(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
+                    const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin,
+                    uint32_t row_end, uint32_t* out_dev, uint64_t* bytes_dev, void* stream) {
+    vr::KView v;
+    int rc = make_view(s, cam, lit, translation, scale, width, height, v);
+    if (rc) return rc;
+    if (row_begin > row_end || row_end > height) return fail(VR_E_INVALID, "bad row range");
+    if (!out_dev || !bytes_dev) return fail(VR_E_INVALID, "NULL device buffer");
+    v.row0 = row_begin;
+    v.band_rows = std::max(1u, row_end - row_begin);
+    v.rank = 0; v.nranks = 1;
+    v.local_rows = row_end - row_begin;
+    v.out = out_dev;
+    v.bytes = (unsigned long long*)bytes_dev;
+    return launch(s, algo, true, v, stream);
+}
+
+int vr_pack_rgb8(const uint32_t* words_dev, uint8_t* rgb_dev, uint64_t n_pixels, void* stream) {
+    if (n_pixels && (!words_dev || !rgb_dev)) return fail(VR_E_INVALID, "NULL device buffer");
+    hipError_t e = vr::launch_pack_rgb8(words_dev, rgb_dev, n_pixels, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "pack_rgb8 launch");
+    return VR_OK;
+}
+
+int vr_synth_generate(const vr_synth_params* p, int32_t* xyz, uint32_t* rgb, size_t capacity, size_t* n_out) {
+    if (!p || !n_out) return fail(VR_E_INVALID, "NULL argument");
+    if (p->n == 0 || p->n % 64 || p->n > 1024) return fail(VR_E_INVALID, "grid side must be a multiple of 64 in [64,1024]");
+    if (xyz && !rgb) return fail(VR_E_INVALID, "rgb NULL");
+    const uint32_t NR = p->n / 64, NC = p->n / 8;
+    size_t cnt = 0;
+    for (uint32_t rz = 0; rz < NR; ++rz)
+        for (uint32_t ry = 0; ry < NR; ++ry)
+            for (uint32_t rx = 0; rx < NR; ++rx) {
+                if (!draw(p->seed, 0, rx + ry * NR + rz * NR * NR, p->p_region)) continue;
+                for (uint32_t cz = rz * 8; cz < rz * 8 + 8; ++cz)
+                    for (uint32_t cy = ry * 8; cy < ry * 8 + 8; ++cy)
+                        for (uint32_t cx = rx * 8; cx < rx * 8 + 8; ++cx) {
+                            if (!draw(p->seed, 1, cx + cy * NC + (uint64_t)cz * NC * NC, p->p_cluster)) continue;
+                            for (uint32_t z = cz * 8; z < cz * 8 + 8; ++z)
+                                for (uint32_t y = cy * 8; y < cy * 8 + 8; ++y)
+                                    for (uint32_t x = cx * 8; x < cx * 8 + 8; ++x) {
+                                        uint64_t key = ((uint64_t)x << 20) | (y << 10) | z;
+                                        if (!draw(p->seed, 2, key, p->p_voxel)) continue;
+                                        if (xyz) {
+                                            if (cnt >= capacity) return fail(VR_E_INVALID, "capacity too small");
+                                            xyz[3 * cnt] = (int32_t)x; xyz[3 * cnt + 1] = (int32_t)y; xyz[3 * cnt + 2] = (int32_t)z;
+                                            rgb[cnt] = (uint32_t)(splitmix64((p->seed << 34) | (3ull << 32) | key) & 0xFFFFFFu);
+                                        }
+                                        ++cnt;
+                                    }
+                        }
+            }
+    *n_out = cnt;
+    return VR_OK;
+}
+
+int vr_vox_read(const char* path, int32_t* xyz, uint32_t* rgb, size_t capacity, size_t* n_out) {
+    if (!path || !n_out) return fail(VR_E_INVALID, "NULL argument");
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(VR_E_IO, std::string("cannot open ") + path + ": " + std::strerror(errno));
+    std::string line;
+    size_t cnt = 0, lineno = 0;
+    char buf[1 << 16];
+    int rc = VR_OK;
+    auto process = [&](const std::string& ln) -> int {
+        ++lineno;
+        // Destructure comma separated values, skipping empty fields (find_first_not_of(",")).
+        const char* p = ln.data();
+        const char* e = p + ln.size();
+        const char* fb[4] = {nullptr, nullptr, nullptr, nullptr};
+        const char* fe[4] = {nullptr, nullptr, nullptr, nullptr};
+        int nf = 0;
+        while (p < e) {
+            while (p < e && *p == ',') ++p;
+            if (p >= e) break;
+            const char* q = p;
+            while (q < e && *q != ',') ++q;
+            if (nf < 4) { fb[nf] = p; fe[nf] = q; }
+            ++nf;
+            p = q;
+        }
+        if (nf <= 3) return VR_OK;                  // lineEntries.size() > 3 (VoxelFile.cuh:25)
+        int32_t v[4];
+        for (int i = 0; i < 4; ++i)
+            if (!stoi_like(fb[i], fe[i], &v[i]))
+                return fail(VR_E_PARSE, std::string(path) + ":" + std::to_string(lineno) + ": std::stoi would throw");
+        if (xyz) {
+            if (cnt >= capacity) return fail(VR_E_INVALID, "capacity too small");
+            xyz[3 * cnt] = v[0]; xyz[3 * cnt + 1] = v[1]; xyz[3 * cnt + 2] = v[2];
+            rgb[cnt] = (uint32_t)v[3];
+        }
+        ++cnt;
+        return VR_OK;
+    };
+    size_t got;
+    while ((got = std::fread(buf, 1, sizeof buf, f)) > 0 && rc == VR_OK) {
+        for (size_t i = 0; i < got && rc == VR_OK; ++i) {
+            if (buf[i] == '\n') { rc = process(line); line.clear(); }
+            else line.push_back(buf[i]);
+        }
+    }
+    if (rc == VR_OK && !line.empty()) rc = process(line);
+    std::fclose(f);
+    if (rc) return rc;
+    *n_out = cnt;
+    return VR_OK;
+}
+
+int vr_vox_write(const char* path, const int32_t* xyz, const uint32_t* rgb, size_t n) {
+    if (!path || (n && (!xyz || !rgb))) return fail(VR_E_INVALID, "NULL argument");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(VR_E_IO, std::string("cannot open ") + path + ": " + std::strerror(errno));
+    for (size_t i = 0; i < n; ++i)
+        std::fprintf(f, "%d,%d,%d,%d\n", xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], (int32_t)rgb[i]);
+    if (std::fclose(f) != 0) return fail(VR_E_IO, std::string("write failed: ") + path);
+    return VR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,54 @@
+// vr_internal.h -- layouts shared by the host builder (vr_host.cpp) and the
+// HIP kernels (vr_march.hip).  See DESIGN.md "Data layout in HBM".
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vr {
+
+constexpr uint32_t kEmpty = 1u << 30;        // EMPTY_KEY == EMPTY_VAL (VoxelFunctions.cuh:20-21)
+constexpr uint32_t kNone = 0xFFFFFFFFu;      // null region / null cluster in the tables
+constexpr int32_t kBlock = 64;               // BLOCK_SIZE (VoxelFunctions.cuh:24)
+constexpr uint32_t kIterBudget = 65536u;     // per-pixel hang guard
+
+// Device view of one immutable scene.  All offsets are 32-bit word indices.
+//  region_slot[D^3]          : region index r, or kNone (null StorageStructure*)
+//  VCS   : vcs_dir[r*512+cid]: word offset of the cluster block in vcs_pool,
+//                              or kNone (VoxelClusterStore::deviceBlockMemAddress)
+//          vcs_pool block    : [n][key_0..key_{n-1}][val_0..val_{n-1}], keys
+//                              ascending (SoA form of VoxelClusterStore.cuh:61-76)
+//  Cuckoo: ht_meta[r]        : {base, M, prime, offset}
+//          ht_slots[base+i]  : table 1 slot i {key, value};
+//          ht_slots[base+M+i]: table 2 slot i {key, value}; empty key = kEmpty
+struct KScene {
+    const uint32_t* region_slot;
+    const uint32_t* vcs_dir;
+    const uint32_t* vcs_pool;
+    const uint4* ht_meta;
+    const uint2* ht_slots;
+    uint32_t D;
+    int32_t min_coord;
+};
+
+// Per-launch view: camera, lighting, scene transform and the row mapping.
+// Local row l of the output maps to frame row
+//   row0 + ((l / band_rows) * nranks + rank) * band_rows + (l % band_rows).
+struct KView {
+    float llc[3], hor[3], ver[3], org[3];
+    float L[3], LC[3], LP[3];
+    float translation[3];
+    float scale_f;
+    int32_t use_point_light, use_shadows;
+    uint32_t W, H;
+    uint32_t row0, band_rows, rank, nranks, local_rows;
+    uint32_t* out;
+    unsigned long long* bytes;
+};
+
+// Launch one render (defined in vr_march.hip).
+hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,
+                        hipStream_t stream);
+hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);
+
+}  // namespace vr

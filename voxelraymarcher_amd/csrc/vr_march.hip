@@ -1,0 +1,594 @@
+// vr_march.hip -- the per-pixel voxel ray march for gfx950 (CDNA4).
+//
+// One lane per pixel; one wave64 = one 8x8 pixel tile (the reference's 8x8
+// CUDA block, Main.cu:109-111, but as a single wavefront so the tile's rays
+// walk the same clusters together); 4 waves (2x2 tiles) per 256-thread
+// workgroup.  Templated on {store, algorithm, count}: no virtual calls, no
+// function pointers (the reference's StorageStructure vtable,
+// StorageStructure.cuh:12-56, and nextXFunc pointers, Renderer.cuh:263-265,
+// become compile-time branches).
+//
+// Arithmetic follows the reference expression by expression (file:line in
+// each function) under the FP policy of SURVEY.md 8(c): -ffp-contract=off,
+// correctly rounded '/' and sqrtf, fminf/fmaxf, truncating saturating
+// float->int with NaN -> 0, wrapping int arithmetic (-fwrapv).  The
+// shadow ray of a hit is evaluated after the primary walk returns instead of
+// from inside it (Renderer.cuh:315,737,821,...): the shadow result depends
+// only on (hit origin, region, shadow algorithm), so the pixel is identical.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "vr_internal.h"
+
+namespace vr {
+namespace {
+
+constexpr float kEps = 0.0001f;               // EPSILON (VoxelFunctions.cuh:19)
+constexpr float kInf = __builtin_huge_valf();
+
+enum { STORE_VCS = 0, STORE_HASH = 1 };
+enum { ALGO_LONGEST = 0, ALGO_ORIGINAL = 1 };
+
+struct f3 { float x, y, z; };
+struct i3 { int32_t x, y, z; };
+
+__device__ __forceinline__ f3 mk(float a, float b, float c) { return f3{a, b, c}; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }   // Vector3.cuh:106
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }   // :112
+__device__ __forceinline__ f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }   // :118
+__device__ __forceinline__ f3 scl(float t, f3 a) { return f3{t * a.x, t * a.y, t * a.z}; }      // :130,142
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }  // :148
+__device__ __forceinline__ f3 unit(f3 a) {                                                         // :162, :79
+    float len = sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
+    return f3{a.x / len, a.y / len, a.z / len};
+}
+__device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+
+// Runtime axis select without private-memory arrays.
+__device__ __forceinline__ float comp(f3 v, uint32_t a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+__device__ __forceinline__ int32_t geti(i3 v, uint32_t a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+__device__ __forceinline__ void seti(i3& v, uint32_t a, int32_t val) {
+    v.x = a == 0 ? val : v.x;
+    v.y = a == 1 ? val : v.y;
+    v.z = a == 2 ? val : v.z;
+}
+__device__ __forceinline__ void setf(f3& v, uint32_t a, float val) {
+    v.x = a == 0 ? val : v.x;
+    v.y = a == 1 ? val : v.y;
+    v.z = a == 2 ? val : v.z;
+}
+
+// static_cast<int32_t>(float) with CUDA device semantics (cvt.rzi.s32.f32).
+__device__ __forceinline__ int32_t f2i(float f) {
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return INT32_MAX;
+    if (f <= -2147483648.0f) return INT32_MIN;
+    return (int32_t)f;
+}
+__device__ __forceinline__ uint32_t f2u(float f) {
+    if (f != f || f <= 0.0f) return 0u;
+    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)f;
+}
+
+// CuckooHashTable::hashFunc1 / hashFunc2 (CuckooHashTable.cuh:181-202),
+// int arithmetic with arithmetic right shifts.
+__device__ __forceinline__ uint32_t hash1(uint32_t k, uint32_t offset) {
+    k = (k + 0x7ed55d16u) + (k << 12);
+    k = (k ^ 0xc761c23cu) ^ (uint32_t)((int32_t)k >> 19);
+    k = (k + 0x165667b1u) + (k << 5);
+    k = (k + 0xd3a2646cu) ^ (k << 9);
+    k = (k + 0xfd7046c5u) + (k << 3);
+    k = (k ^ 0xb55a4f09u) ^ (uint32_t)((int32_t)k >> 16);
+    return k + offset;
+}
+__device__ __forceinline__ uint32_t hash2(uint32_t k, uint32_t prime) {
+    k = (k ^ 61u) ^ (uint32_t)((int32_t)k >> 16);
+    k = k + (k << 3);
+    k = k ^ (uint32_t)((int32_t)k >> 4);
+    k = k * prime;
+    k = k ^ (uint32_t)((int32_t)k >> 15);
+    return k;
+}
+
+struct Hit {
+    uint32_t lit;       // lit colour before the shadow multiply
+    f3 so;              // shadow-ray origin (region-local)
+    i3 region;          // currentRegion at the hit
+    bool longest;       // isInShadowRayMarchVoxelSceneLongestAxis vs ...Original
+};
+
+template <int STORE, bool COUNT>
+struct Walker {
+    const KScene& s;
+    const KView& v;
+    uint32_t iters = 0;
+    bool aborted = false;
+    uint32_t bytes = 0;
+
+    __device__ Walker(const KScene& s_, const KView& v_) : s(s_), v(v_) {}
+
+    __device__ __forceinline__ void count(uint32_t b) {
+        if (COUNT) bytes += b;
+    }
+    __device__ __forceinline__ bool tick() {
+        if (aborted) return false;
+        if (++iters > kIterBudget) { aborted = true; return false; }
+        return true;
+    }
+
+    // VoxelScene::isRayInScene / getRegionStorageStructure (Renderer.cuh:29-44)
+    __device__ __forceinline__ bool in_scene(i3 r) const {
+        uint32_t mc = (uint32_t)s.min_coord;
+        return ((uint32_t)r.x - mc) < s.D && ((uint32_t)r.y - mc) < s.D && ((uint32_t)r.z - mc) < s.D;
+    }
+    __device__ __forceinline__ uint32_t region_at(i3 r) {
+        uint32_t mc = (uint32_t)s.min_coord;
+        uint32_t ux = (uint32_t)r.x - mc, uy = (uint32_t)r.y - mc, uz = (uint32_t)r.z - mc;
+        count(4);
+        return s.region_slot[ux + uy * s.D + uz * s.D * s.D];
+    }
+
+    // doesVoxelSpaceExist (StorageStructure.cuh:29-32,49-52) ->
+    // VoxelClusterStore::doesClusterExist (VoxelClusterStore.cuh:93-99).
+    // Returns the cluster block offset (VCS) or 0 (hashtable), kNone = absent.
+    __device__ __forceinline__ uint32_t exists(uint32_t reg, int32_t x, int32_t y, int32_t z) {
+        if (STORE == STORE_HASH) return 0u;
+        count(4);
+        uint32_t c = (((uint32_t)x >> 3) << 6) | (((uint32_t)y >> 3) << 3) | ((uint32_t)z >> 3);
+        int32_t cid = (int32_t)(int16_t)(uint16_t)c;      // `short` getVoxelClusterID
+        if (cid < 0 || cid >= 512) return kNone;          // past the reference's directory
+        return s.vcs_dir[reg * 512u + (uint32_t)cid];
+    }
+
+    // VoxelClusterStore::lookupVoxel / performBinarySearch (VoxelClusterStore.cuh:101-135),
+    // CuckooHashTable::lookupVoxel (CuckooHashTable.cuh:59-76).
+    __device__ __forceinline__ uint32_t lookup(uint32_t reg, uint32_t blk, int32_t x, int32_t y, int32_t z) {
+        uint32_t key = ((uint32_t)x << 20) | ((uint32_t)y << 10) | (uint32_t)z;   // generate3DPoint
+        if (STORE == STORE_VCS) {
+            const uint32_t* b = s.vcs_pool + blk;
+            uint32_t n = b[0];
+            count(4);
+            int32_t low = 0, high = (int32_t)n - 1;
+            while (low <= high) {
+                int32_t mid = low + ((high - low) >> 1);
+                uint32_t k = b[1 + mid];
+                count(4);
+                if (k == key) { count(4); return b[1 + n + (uint32_t)mid]; }
+                if (k < key) low = mid + 1; else high = mid - 1;
+            }
+            return kEmpty;
+        } else {
+            uint4 m = s.ht_meta[reg];          // {base, M, prime, offset}
+            uint32_t s1 = hash1(key, m.w) % m.y;
+            count(4);
+            uint2 e = s.ht_slots[m.x + s1];
+            if (e.x == key) { count(4); return e.y; }
+            uint32_t s2 = hash2(key, m.z) % m.y;
+            count(4);
+            e = s.ht_slots[m.x + m.y + s2];
+            if (e.x == key) { count(4); return e.y; }
+            return kEmpty;
+        }
+    }
+
+    // applyLighting / applyDirectionalLightingToColor / applyPointLightingToColor
+    // (Renderer.cuh:57-86,249-258), colour packing (VoxelFunctions.cuh:69-83).
+    __device__ __forceinline__ uint32_t lighting(uint32_t col, f3 n, f3 rwp, f3 ro) const {
+        f3 LC = ld3(v.LC);
+        f3 c = mk((float)(col >> 16) / 255.0f, (float)((col >> 8) & 0xFFu) / 255.0f, (float)(col & 0xFFu) / 255.0f);
+        f3 r;
+        if (v.use_point_light) {
+            f3 p2l = sub(ld3(v.LP), add(rwp, ro));
+            float dist = sqrtf(p2l.x * p2l.x + p2l.y * p2l.y + p2l.z * p2l.z);
+            f3 ldir = unit(p2l);
+            float att = 1.0f / (1.0f + 0.045f * dist + 0.0075f * (dist * dist));
+            float diff = fmaxf(dot3(n, ldir), 0.0f);
+            r = mul(scl(att, scl(diff, LC)), c);
+        } else {
+            float diff = fmaxf(dot3(n, ld3(v.L)), 0.0f);
+            r = mul(c, scl(diff, LC));
+        }
+        uint32_t R = f2u(r.x * 255.0f), G = f2u(r.y * 255.0f), B = f2u(r.z * 255.0f);
+        return (R << 16) | (G << 8) | B;
+    }
+
+    // getNormalFromTValues (Renderer.cuh:237-247)
+    __device__ __forceinline__ static f3 normal_from_t(float tX, float tY, float tZ, float tMin, f3 d) {
+        if (tX == tMin) return mk(copysignf(1.0f, -d.x), 0.0f, 0.0f);
+        if (tY == tMin) return mk(0.0f, copysignf(1.0f, -d.y), 0.0f);
+        return mk(0.0f, 0.0f, copysignf(1.0f, -d.z));
+    }
+
+    __device__ __forceinline__ static bool in_region(f3 o) {               // Renderer.cuh:93-98
+        return o.x >= 0.0f && o.x < 64.0f && o.y >= 0.0f && o.y < 64.0f && o.z >= 0.0f && o.z < 64.0f;
+    }
+    __device__ __forceinline__ static bool grid_in_region(int32_t a, int32_t b, int32_t c) {   // :436-439
+        return (uint32_t)a < 64u && (uint32_t)b < 64u && (uint32_t)c < 64u;
+    }
+
+    // Region advance (e.g. Renderer.cuh:421-429).
+    __device__ __forceinline__ static void advance_region(i3& cr, f3& o) {
+        int32_t dx = f2i(floorf(o.x / 64.0f)), dy = f2i(floorf(o.y / 64.0f)), dz = f2i(floorf(o.z / 64.0f));
+        cr.x += dx; cr.y += dy; cr.z += dz;
+        o = sub(o, mk((float)(dx * kBlock), (float)(dy * kBlock), (float)(dz * kBlock)));
+    }
+
+    // Null-region skip body (Renderer.cuh:386-409; guarded form :187-210).
+    template <bool GUARDED>
+    __device__ __forceinline__ bool skip_null(i3& cr, f3& o, f3 d, uint32_t& reg) {
+        float nx = d.x > 0.0f ? 64.0f + kEps : 0.0f - kEps;
+        float ny = d.y > 0.0f ? 64.0f + kEps : 0.0f - kEps;
+        float nz = d.z > 0.0f ? 64.0f + kEps : 0.0f - kEps;
+        float tX, tY, tZ;
+        if (GUARDED) {
+            tX = d.x != 0.0f ? (nx - o.x) / d.x : kInf;
+            tY = d.y != 0.0f ? (ny - o.y) / d.y : kInf;
+            tZ = d.z != 0.0f ? (nz - o.z) / d.z : kInf;
+        } else {
+            tX = (nx - o.x) / d.x;
+            tY = (ny - o.y) / d.y;
+            tZ = (nz - o.z) / d.z;
+        }
+        float tMin = fminf(tX, fminf(tY, tZ));
+        o = add(o, scl(tMin, d));
+        advance_region(cr, o);
+        if (!in_scene(cr)) return false;
+        reg = region_at(cr);
+        return true;
+    }
+
+    // rayMarchVoxelGrid (Renderer.cuh:260-336) and, SHADOW, shadowRayMarchVoxelGrid (:100-172).
+    template <bool SHADOW>
+    __device__ bool grid_original(f3& o, f3 d, uint32_t reg, f3 rwp, i3 cr, Hit& h) {
+        const bool px = d.x > 0.0f, py = d.y > 0.0f, pz = d.z > 0.0f;
+        float nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
+        float nY = py ? ceilf(o.y) + kEps : floorf(o.y) - kEps;
+        float nZ = pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps;
+        float tX, tY, tZ;
+        if (SHADOW) {
+            tX = d.x != 0.0f ? (nX - o.x) / d.x : kInf;
+            tY = d.y != 0.0f ? (nY - o.y) / d.y : kInf;
+            tZ = d.z != 0.0f ? (nZ - o.z) / d.z : kInf;
+        } else {
+            tX = (nX - o.x) / d.x;
+            tY = (nY - o.y) / d.y;
+            tZ = (nZ - o.z) / d.z;
+        }
+        float tMin = fminf(tX, fminf(tY, tZ));
+        o = add(o, scl(tMin + kEps, d));
+        while (in_region(o)) {
+            if (!tick()) return false;
+            int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
+            uint32_t blk = exists(reg, vx, vy, vz);
+            if (blk == kNone) {
+                // cluster skip; block-scoped t values (stale outer ones)
+                int32_t cx = px ? ((vx / 8) + 1) * 8 : (vx / 8) * 8;
+                int32_t cy = py ? ((vy / 8) + 1) * 8 : (vy / 8) * 8;
+                int32_t cz = pz ? ((vz / 8) + 1) * 8 : (vz / 8) * 8;
+                float sX, sY, sZ;
+                if (SHADOW) {
+                    sX = d.x != 0.0f ? ((float)cx - o.x) / d.x : kInf;
+                    sY = d.y != 0.0f ? ((float)cy - o.y) / d.y : kInf;
+                    sZ = d.z != 0.0f ? ((float)cz - o.z) / d.z : kInf;
+                } else {
+                    sX = ((float)cx - o.x) / d.x;
+                    sY = ((float)cy - o.y) / d.y;
+                    sZ = ((float)cz - o.z) / d.z;
+                }
+                float sMin = fminf(sX, fminf(sY, sZ));
+                o = add(o, scl(sMin + kEps, d));
+                continue;
+            }
+            uint32_t col = lookup(reg, blk, vx, vy, vz);
+            if (col != kEmpty) {
+                if (!SHADOW) {
+                    h.lit = lighting(col, normal_from_t(tX, tY, tZ, tMin, d), rwp, o);
+                    h.so = o;
+                    h.region = cr;
+                    h.longest = false;
+                }
+                return true;
+            }
+            nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
+            nY = py ? ceilf(o.y) + kEps : floorf(o.y) - kEps;
+            nZ = pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps;
+            if (SHADOW) {
+                tX = d.x != 0.0f ? (nX - o.x) / d.x : kInf;
+                tY = d.y != 0.0f ? (nY - o.y) / d.y : kInf;
+                tZ = d.z != 0.0f ? (nZ - o.z) / d.z : kInf;
+            } else {
+                tX = (nX - o.x) / d.x;
+                tY = (nY - o.y) / d.y;
+                tZ = (nZ - o.z) / d.z;
+            }
+            tMin = fminf(tX, fminf(tY, tZ));
+            o = add(o, scl(tMin + kEps, d));
+        }
+        return false;
+    }
+
+    // State of one longest-axis region walk (Renderer.cuh:760-915 / :495-631).
+    struct LA {
+        f3 old_o, ray_o, ds;
+        i3 g, ad;
+        uint32_t L, M, S;
+    };
+
+    // performVoxelSpaceJump (Renderer.cuh:696-751) / performShadowVoxelSpaceJump (:441-492).
+    // Returns 0 = EMPTY_VAL (left region / aborted), 1 = hit, 2 = CONTINUE_VAL.
+    template <bool SHADOW>
+    __device__ int jump(f3& oo, LA& a, uint32_t reg, f3 rwp, i3 cr, Hit& h) {
+        float tX = 0.0f, tY = 0.0f, tZ = 0.0f, tMin = 0.0f;
+        uint32_t blk;
+        while ((blk = exists(reg, a.g.x, a.g.y, a.g.z)) == kNone) {
+            if (!tick()) return 0;
+            int32_t nx = a.ds.x > 0.0f ? ((a.g.x / 8) + 1) * 8 : (a.g.x / 8) * 8;
+            int32_t ny = a.ds.y > 0.0f ? ((a.g.y / 8) + 1) * 8 : (a.g.y / 8) * 8;
+            int32_t nz = a.ds.z > 0.0f ? ((a.g.z / 8) + 1) * 8 : (a.g.z / 8) * 8;
+            tX = ((float)nx - a.old_o.x) / a.ds.x;
+            tY = ((float)ny - a.old_o.y) / a.ds.y;
+            tZ = ((float)nz - a.old_o.z) / a.ds.z;
+            tMin = fminf(tX, fminf(tY, tZ)) + kEps;
+            a.old_o = add(a.old_o, scl(tMin, a.ds));
+            a.g = i3{f2i(floorf(a.old_o.x)), f2i(floorf(a.old_o.y)), f2i(floorf(a.old_o.z))};
+            if (!grid_in_region(a.g.x, a.g.y, a.g.z)) {
+                oo = a.old_o;
+                return 0;
+            }
+        }
+        uint32_t col = lookup(reg, blk, a.g.x, a.g.y, a.g.z);
+        if (col != kEmpty) {
+            if (!SHADOW) {
+                h.lit = lighting(col, normal_from_t(tX, tY, tZ, tMin, a.ds), rwp, a.old_o);
+                h.so = a.old_o;
+                h.region = cr;
+                h.longest = true;
+            }
+            return 1;
+        }
+        float oL = comp(a.old_o, a.L), dL = comp(a.ds, a.L);
+        float tNext = dL > 0.0f ? (ceilf(oL) - oL) / dL : (floorf(oL) - oL) / dL;
+        a.ray_o = add(a.old_o, scl(tNext + kEps, a.ds));
+        seti(a.ad, a.M, f2i(comp(a.ray_o, a.M)) - geti(a.g, a.M));
+        seti(a.ad, a.S, f2i(comp(a.ray_o, a.S)) - geti(a.g, a.S));
+        return 2;
+    }
+
+    // One "grid += diff; exists? else jump; lookup; hit" block
+    // (Renderer.cuh:807-901 / :542-617).  0 = go on, 1 = return *res, 2 = continue.
+    template <bool SHADOW>
+    __device__ int axis_step(f3& oo, LA& a, uint32_t axis, bool long_axis, uint32_t reg, f3 rwp, i3 cr,
+                             Hit& h, bool& res) {
+        seti(a.g, axis, geti(a.g, axis) + geti(a.ad, axis));
+        uint32_t blk = exists(reg, a.g.x, a.g.y, a.g.z);
+        if (blk == kNone) {
+            int jr = jump<SHADOW>(oo, a, reg, rwp, cr, h);
+            if (aborted) { res = false; return 1; }
+            if (jr != 2) { res = jr == 1; return 1; }
+            return 2;
+        }
+        uint32_t col = lookup(reg, blk, a.g.x, a.g.y, a.g.z);
+        if (col != kEmpty) {
+            if (!SHADOW) {
+                f3 n = mk(0.0f, 0.0f, 0.0f);
+                setf(n, axis, copysignf(1.0f, -comp(a.ds, axis)));
+                f3 hit;
+                if (long_axis) {
+                    hit = a.ray_o;
+                } else {  // getLocalHitLocation (Renderer.cuh:753-758)
+                    float o = comp(a.old_o, axis), dd = comp(a.ds, axis);
+                    float t = dd > 0.0f ? (ceilf(o) - o) / dd : (floorf(o) - o) / dd;
+                    hit = add(a.old_o, scl(t, a.ds));
+                }
+                h.lit = lighting(col, n, rwp, hit);
+                h.so = hit;
+                h.region = cr;
+                h.longest = true;
+            }
+            res = true;
+            return 1;
+        }
+        return 0;
+    }
+
+    // rayMarchVoxelGridLongestAxis (Renderer.cuh:760-915) /
+    // shadowRayMarchVoxelGridLongestAxis (:495-631).
+    template <bool SHADOW>
+    __device__ bool grid_longest(f3& oo, f3 od, uint32_t reg, f3 rwp, i3 cr, Hit& h) {
+        LA a;
+        // Ray::convertRayToLongestAxisDirection (Ray.cuh:19-71)
+        float ax = fabsf(od.x), ay = fabsf(od.y), az = fabsf(od.z), k;
+        if (ax > ay && ax > az) {
+            a.L = 0; a.M = ay > az ? 1 : 2; a.S = ay > az ? 2 : 1; k = 1.0f / ax;
+        } else if (ay > az) {
+            a.L = 1; a.M = ax > az ? 0 : 2; a.S = ax > az ? 2 : 0; k = 1.0f / ay;
+        } else {
+            a.L = 2; a.M = ax > ay ? 0 : 1; a.S = ax > ay ? 1 : 0; k = 1.0f / az;
+        }
+        a.ds = scl(k, od);
+        a.old_o = oo;
+        a.g = i3{f2i(oo.x), f2i(oo.y), f2i(oo.z)};
+        a.ad = i3{0, 0, 0};
+        int32_t adL = comp(od, a.L) < 0.0f ? -1 : 1;
+        seti(a.ad, a.L, adL);
+        float gL = (float)geti(a.g, a.L), oL = comp(oo, a.L);
+        float t = adL > 0 ? (gL + kEps + 1.0f - oL) / (float)adL : (gL - kEps - oL) / (float)adL;
+        a.ray_o = add(a.old_o, scl(t, a.ds));
+        seti(a.ad, a.M, f2i(comp(a.ray_o, a.M)) - geti(a.g, a.M));
+        seti(a.ad, a.S, f2i(comp(a.ray_o, a.S)) - geti(a.g, a.S));
+        const bool mid_floor = comp(a.ds, a.M) < 0.0f;   // decimalToIntFunc (:784)
+        bool res = false;
+        while (grid_in_region(geti(a.g, a.L) + geti(a.ad, a.L), geti(a.g, a.M) + geti(a.ad, a.M),
+                              geti(a.g, a.S) + geti(a.ad, a.S))) {
+            if (!tick()) return false;
+            int r;
+            int32_t adM = geti(a.ad, a.M), adS = geti(a.ad, a.S);
+            if (adS != 0 && adM != 0) {
+                float om = comp(a.old_o, a.M);
+                float t1 = ((mid_floor ? floorf(om) : ceilf(om)) - om) / comp(a.ds, a.M);
+                float sp = comp(a.old_o, a.S) + comp(a.ds, a.S) * t1;
+                int32_t sd = f2i(floorf(sp)) - geti(a.g, a.S);
+                uint32_t a0 = sd != 0 ? a.S : a.M, a1 = sd != 0 ? a.M : a.S;
+                r = axis_step<SHADOW>(oo, a, a0, false, reg, rwp, cr, h, res);
+                if (r == 1) return res;
+                if (r == 2) continue;
+                r = axis_step<SHADOW>(oo, a, a1, false, reg, rwp, cr, h, res);
+                if (r == 1) return res;
+                if (r == 2) continue;
+            } else if (adM != 0) {
+                r = axis_step<SHADOW>(oo, a, a.M, false, reg, rwp, cr, h, res);
+                if (r == 1) return res;
+                if (r == 2) continue;
+            } else if (adS != 0) {
+                r = axis_step<SHADOW>(oo, a, a.S, false, reg, rwp, cr, h, res);
+                if (r == 1) return res;
+                if (r == 2) continue;
+            }
+            r = axis_step<SHADOW>(oo, a, a.L, true, reg, rwp, cr, h, res);
+            if (r == 1) return res;
+            if (r == 2) continue;
+            a.old_o = a.ray_o;
+            a.ray_o = add(a.ray_o, a.ds);
+            seti(a.ad, a.M, f2i(comp(a.ray_o, a.M)) - geti(a.g, a.M));
+            seti(a.ad, a.S, f2i(comp(a.ray_o, a.S)) - geti(a.g, a.S));
+        }
+        oo = a.old_o;     // Renderer.cuh:912 (direction of originalRay kept)
+        return grid_original<SHADOW>(oo, od, reg, rwp, cr, h);
+    }
+
+    // rayMarchVoxelScene (Renderer.cuh:338-434) / rayMarchVoxelSceneLongestAxis (:917-1010).
+    template <int ALGO>
+    __device__ bool primary(f3 wo, f3 wd, Hit& h) {
+        f3 tr = ld3(v.translation);
+        f3 so = scl(v.scale_f, sub(wo, tr));      // Ray::convertRayToLocalSpace (Ray.cuh:14-17)
+        f3 d = wd;
+        i3 cr{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
+        while (!in_scene(cr)) {                   // entry clip (:349-373)
+            if (!tick()) return false;
+            int32_t hi = (int32_t)(s.D + (uint32_t)s.min_coord), lo = s.min_coord;
+            int32_t nx = d.x < 0.0f ? hi : lo, ny = d.y < 0.0f ? hi : lo, nz = d.z < 0.0f ? hi : lo;
+            float tX = ((float)(nx * kBlock) - so.x) / d.x;
+            float tY = ((float)(ny * kBlock) - so.y) / d.y;
+            float tZ = ((float)(nz * kBlock) - so.z) / d.z;
+            if (tX <= 0.0f) tX = kInf;
+            if (tY <= 0.0f) tY = kInf;
+            if (tZ <= 0.0f) tZ = kInf;
+            float tMin = fminf(tX, fminf(tY, tZ));
+            if (tMin == kInf) return false;
+            so = add(so, scl(tMin + kEps, d));
+            cr = i3{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
+        }
+        f3 o = sub(so, mk((float)(cr.x * kBlock), (float)(cr.y * kBlock), (float)(cr.z * kBlock)));
+        while (in_scene(cr)) {
+            if (!tick()) return false;
+            uint32_t reg = region_at(cr);
+            while (reg == kNone) {
+                if (!tick()) return false;
+                if (!skip_null<false>(cr, o, d, reg)) return false;
+            }
+            f3 rwp = add(tr, mk((float)(cr.x * kBlock), (float)(cr.y * kBlock), (float)(cr.z * kBlock)));
+            bool hit = ALGO == ALGO_ORIGINAL ? grid_original<false>(o, d, reg, rwp, cr, h)
+                                             : grid_longest<false>(o, d, reg, rwp, cr, h);
+            if (aborted) return false;
+            if (hit) return true;
+            advance_region(cr, o);
+        }
+        return false;
+    }
+
+    // isInShadowOriginalRayMarch (Renderer.cuh:174-235) /
+    // isInShadowRayMarchVoxelSceneLongestAxis (:633-694).
+    template <bool LONGEST>
+    __device__ bool shadow(f3 o, i3 cr) {
+        f3 d = ld3(v.L);
+        Hit dummy;
+        while (in_scene(cr)) {
+            if (!tick()) return false;
+            uint32_t reg = region_at(cr);
+            while (reg == kNone) {
+                if (!tick()) return false;
+                if (!skip_null<!LONGEST>(cr, o, d, reg)) return false;
+            }
+            bool hit = LONGEST ? grid_longest<true>(o, d, reg, mk(0.0f, 0.0f, 0.0f), cr, dummy)
+                               : grid_original<true>(o, d, reg, mk(0.0f, 0.0f, 0.0f), cr, dummy);
+            if (aborted) return false;
+            if (hit) return true;
+            advance_region(cr, o);
+        }
+        return false;
+    }
+};
+
+// rayMarchSceneOriginal / rayMarchSceneJumpAxis (Renderer.cuh:1033-1063).
+template <int STORE, int ALGO, bool COUNT>
+__global__ __launch_bounds__(256) void march_kernel(KScene s, KView v) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t x = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
+    const uint32_t l = (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
+    uint32_t bytes = 0;
+    if (x < v.W && l < v.local_rows) {
+        const uint32_t band = l / v.band_rows;
+        const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
+        uint32_t col = 0;
+        if (y < v.H) {
+            // calculateWorldRay (Renderer.cuh:1013-1022) + Camera::generateRay (Camera.cuh:25-29)
+            float u = ((float)x + 0.5f) / (float)v.W;
+            float vv = ((float)(v.H - y) + 0.5f) / (float)v.H;
+            f3 ro = add(add(ld3(v.llc), scl(u, ld3(v.hor))), scl(vv, ld3(v.ver)));
+            f3 rd = unit(sub(ro, ld3(v.org)));
+            Walker<STORE, COUNT> w(s, v);
+            Hit h;
+            if (w.template primary<ALGO>(ro, rd, h)) {
+                bool sh = false;
+                if (v.use_shadows)
+                    sh = h.longest ? w.template shadow<true>(h.so, h.region) : w.template shadow<false>(h.so, h.region);
+                col = h.lit * (uint32_t)!sh;
+            }
+            if (w.aborted) col = 0;
+            bytes = w.bytes + 4u;                 // + the pixel write
+        }
+        v.out[(size_t)l * v.W + x] = col;
+    }
+    if (COUNT) {
+        // wave64 reduction, one atomic per wave
+        unsigned long long b = bytes;
+        for (int off = 32; off > 0; off >>= 1) b += __shfl_down(b, off, 64);
+        if (lane == 0 && b) atomicAdd(v.bytes, b);
+    }
+}
+
+__global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __restrict__ rgb, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t c = w[i];
+    rgb[3 * i + 0] = (uint8_t)(c >> 16);
+    rgb[3 * i + 1] = (uint8_t)((c >> 8) & 0xFFu);
+    rgb[3 * i + 2] = (uint8_t)(c & 0xFFu);
+}
+
+}  // namespace
+
+hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream) {
+    dim3 grid((v.W + 15u) / 16u, (v.local_rows + 15u) / 16u);
+    dim3 block(256);
+    if (grid.x == 0 || grid.y == 0) return hipSuccess;
+#define VR_LAUNCH(ST, AL, CT) hipLaunchKernelGGL((march_kernel<ST, AL, CT>), grid, block, 0, stream, s, v)
+    if (store == STORE_VCS) {
+        if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, false); }
+        else { if (count) VR_LAUNCH(STORE_VCS, ALGO_LONGEST, true); else VR_LAUNCH(STORE_VCS, ALGO_LONGEST, false); }
+    } else {
+        if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_HASH, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_HASH, ALGO_ORIGINAL, false); }
+        else { if (count) VR_LAUNCH(STORE_HASH, ALGO_LONGEST, true); else VR_LAUNCH(STORE_HASH, ALGO_LONGEST, false); }
+    }
+#undef VR_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pack_rgb8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, words, rgb, n);
+    return hipGetLastError();
+}
+
+}  // namespace vr

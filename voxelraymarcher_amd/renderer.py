@@ -1,0 +1,297 @@
+"""Host-side interface of the renderer, mirroring the reference's host names.
+
+  StorageType            geometry/VoxelFunctions.cuh:37
+  Camera                 renderer/camera/Camera.cuh:11-29
+  VoxelSceneInfo         renderer/VoxelSceneInfo.cuh:5-15
+  VoxelSceneCPU          geometry/VoxelSceneCPU.cuh:13-131 (insertVoxel, generateVoxelScene)
+  read_voxel_file        geometry/VoxelFile.cuh:9-35
+  setup_constant_values  main/Main.cu:26-42
+  run_raymarching_kernel main/Main.cu:105-163
+
+All compute goes through libvr.so (HIP, gfx950).  Device buffers are torch
+tensors (plumbing only); frames are uint32 tensors of packed 0x00RRGGBB words.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from ctypes import c_int32, c_size_t, c_uint32, c_void_p
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _capi
+from ._capi import check, f3, lib
+
+
+class StorageType(enum.IntEnum):
+    VOXEL_CLUSTER_STORE = _capi.VR_STORE_VCS
+    HASH_TABLE = _capi.VR_STORE_HASHTABLE
+
+
+class RayMarchAlgorithm(enum.IntEnum):
+    LONGEST_AXIS = _capi.VR_ALGO_LONGESTAXIS
+    ORIGINAL = _capi.VR_ALGO_ORIGINAL
+
+
+def parse_storage(name: str) -> StorageType:
+    """processStorageTypeCmdArg (Main.cu:45-55): 'hashtable' else VCS."""
+    return StorageType.HASH_TABLE if name == "hashtable" else StorageType.VOXEL_CLUSTER_STORE
+
+
+def parse_algorithm(name: str) -> RayMarchAlgorithm:
+    """processAlgorithmCmdArg (Main.cu:58-68): 'original' else longest axis."""
+    return RayMarchAlgorithm.ORIGINAL if name == "original" else RayMarchAlgorithm.LONGEST_AXIS
+
+
+class Camera:
+    """Camera(o, lookAt, globalUp, fieldOfView, aspectRatio) (Camera.cuh:11-23), built on the host."""
+
+    def __init__(self, origin, look_at, global_up, field_of_view: float, aspect_ratio: float):
+        self.raw = _capi.VrCamera()
+        check(lib().vr_camera_make(f3(origin), f3(look_at), f3(global_up), float(field_of_view),
+                                   float(aspect_ratio), ctypes.byref(self.raw)), "Camera")
+
+    @classmethod
+    def reference(cls, width: int, height: int) -> "Camera":
+        """The hard-coded camera of Main.cu:197-199."""
+        aspect = float(np.float32(width) / np.float32(height))
+        return cls((6.0, 2.0, 6.0), (0.0, 0.0, -1.0), (0.0, 1.0, 0.0), 60.0, aspect)
+
+    def as_floats(self) -> np.ndarray:
+        r = self.raw
+        return np.array([list(r.origin), list(r.lower_left), list(r.horizontal), list(r.vertical),
+                         list(r.forward)], dtype=np.float32)
+
+
+def setup_constant_values(use_shadows: bool = True, use_point_light: bool = False,
+                          light_position=(10.0, 10.0, -10.0)) -> _capi.VrLighting:
+    """setupConstantValues (Main.cu:26-42) -> the lighting block."""
+    lit = _capi.VrLighting()
+    check(lib().vr_lighting_default(ctypes.byref(lit)), "setupConstantValues")
+    lit.use_shadows = int(bool(use_shadows))
+    lit.use_point_light = int(bool(use_point_light))
+    for i in range(3):
+        lit.light_pos[i] = float(light_position[i])
+    return lit
+
+
+@dataclass
+class VoxelSceneInfo:
+    """VoxelSceneInfo(location, scale) (VoxelSceneInfo.cuh:5-15)."""
+    translation: tuple = (0.0, 0.0, 0.0)
+    scale: int = 1
+
+
+class DeviceScene:
+    """One immutable scene resident in HBM (owns the vr_scene handle)."""
+
+    def __init__(self, handle: c_void_p):
+        self._h = handle
+
+    @property
+    def handle(self) -> c_void_p:
+        if not self._h:
+            raise ValueError("scene destroyed")
+        return self._h
+
+    def info(self) -> dict:
+        i = _capi.VrSceneInfo()
+        check(lib().vr_scene_get_info(self.handle, ctypes.byref(i)), "vr_scene_get_info")
+        return {"diameter": i.diameter, "min_coord": i.min_coord, "region_count": i.region_count,
+                "store": StorageType(i.store), "voxel_count": i.voxel_count, "device_bytes": i.device_bytes,
+                "device": i.device}
+
+    def close(self) -> None:
+        if self._h:
+            lib().vr_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def create_scene(xyz: np.ndarray, rgb: np.ndarray, store: StorageType, device: int = 0) -> DeviceScene:
+    """generateVoxelScene(storageType) over the voxels (VoxelSceneCPU.cuh:49-93)."""
+    xyz = np.ascontiguousarray(xyz, dtype=np.int32).reshape(-1, 3)
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint32).reshape(-1)
+    if xyz.shape[0] != rgb.shape[0]:
+        raise ValueError("xyz and rgb lengths differ")
+    h = c_void_p()
+    check(lib().vr_scene_create(int(device), int(store), xyz.ctypes.data_as(ctypes.POINTER(c_int32)),
+                                rgb.ctypes.data_as(ctypes.POINTER(c_uint32)), rgb.shape[0], ctypes.byref(h)),
+          "generateVoxelScene")
+    return DeviceScene(h)
+
+
+class VoxelSceneCPU:
+    """Host-side voxel accumulator (VoxelSceneCPU.cuh:13-46)."""
+
+    def __init__(self):
+        self._xyz: list = []
+        self._rgb: list = []
+
+    def insert_voxel(self, x: int, y: int, z: int, color: int) -> None:
+        self._xyz.append((int(x), int(y), int(z)))
+        self._rgb.append(int(color) & 0xFFFFFFFF)
+
+    insertVoxel = insert_voxel
+
+    def extend(self, xyz: np.ndarray, rgb: np.ndarray) -> None:
+        self._xyz.extend(map(tuple, np.asarray(xyz, dtype=np.int64).reshape(-1, 3).tolist()))
+        self._rgb.extend(np.asarray(rgb, dtype=np.uint64).reshape(-1).tolist())
+
+    def arrays(self):
+        return (np.array(self._xyz, dtype=np.int32).reshape(-1, 3), np.array(self._rgb, dtype=np.uint32))
+
+    def generate_voxel_scene(self, storage_type: StorageType, device: int = 0) -> DeviceScene:
+        xyz, rgb = self.arrays()
+        return create_scene(xyz, rgb, storage_type, device)
+
+    generateVoxelScene = generate_voxel_scene
+
+
+def read_voxel_file(path: str):
+    """VoxelFile::readVoxelFile (VoxelFile.cuh:9-35) -> (xyz int32[n,3], rgb uint32[n])."""
+    n = c_size_t()
+    check(lib().vr_vox_read(path.encode(), None, None, 0, ctypes.byref(n)), "readVoxelFile")
+    xyz = np.zeros((max(n.value, 1), 3), dtype=np.int32)
+    rgb = np.zeros(max(n.value, 1), dtype=np.uint32)
+    check(lib().vr_vox_read(path.encode(), xyz.ctypes.data_as(ctypes.POINTER(c_int32)),
+                            rgb.ctypes.data_as(ctypes.POINTER(c_uint32)), n.value, ctypes.byref(n)), "readVoxelFile")
+    return xyz[: n.value].copy(), rgb[: n.value].copy()
+
+
+def write_voxel_file(path: str, xyz: np.ndarray, rgb: np.ndarray) -> None:
+    xyz = np.ascontiguousarray(xyz, dtype=np.int32).reshape(-1, 3)
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint32).reshape(-1)
+    check(lib().vr_vox_write(path.encode(), xyz.ctypes.data_as(ctypes.POINTER(c_int32)),
+                             rgb.ctypes.data_as(ctypes.POINTER(c_uint32)), rgb.shape[0]), "write_voxel_file")
+
+
+def synth_scene(n: int, p_region: float, p_cluster: float, p_voxel: float, seed: int):
+    """Synthetic counter-hash grid -> (xyz int32[n,3], rgb uint32[n])."""
+    p = _capi.VrSynthParams(int(n), float(p_region), float(p_cluster), float(p_voxel), int(seed))
+    cnt = c_size_t()
+    check(lib().vr_synth_generate(ctypes.byref(p), None, None, 0, ctypes.byref(cnt)), "vr_synth_generate")
+    xyz = np.zeros((max(cnt.value, 1), 3), dtype=np.int32)
+    rgb = np.zeros(max(cnt.value, 1), dtype=np.uint32)
+    check(lib().vr_synth_generate(ctypes.byref(p), xyz.ctypes.data_as(ctypes.POINTER(c_int32)),
+                                  rgb.ctypes.data_as(ctypes.POINTER(c_uint32)), cnt.value, ctypes.byref(cnt)),
+          "vr_synth_generate")
+    return xyz[: cnt.value].copy(), rgb[: cnt.value].copy()
+
+
+def _stream_ptr(stream) -> c_void_p:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return c_void_p(stream.cuda_stream)
+
+
+def _require_u32(out: torch.Tensor, words: int) -> None:
+    if not out.is_cuda or out.dtype != torch.int32 and out.dtype != torch.uint32:
+        raise TypeError("out must be a CUDA int32/uint32 tensor")
+    if not out.is_contiguous() or out.numel() < words:
+        raise ValueError(f"out must be contiguous with >= {words} elements")
+
+
+def run_raymarching_kernel(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera,
+                           lighting: _capi.VrLighting, info: VoxelSceneInfo, width: int, height: int,
+                           out: torch.Tensor | None = None, row_begin: int = 0, row_end: int | None = None,
+                           stream=None) -> torch.Tensor:
+    """Launch the ray march for rows [row_begin,row_end) (Main.cu:105-163); asynchronous."""
+    row_end = height if row_end is None else row_end
+    words = (row_end - row_begin) * width
+    if out is None:
+        out = torch.empty(words, dtype=torch.int32, device=f"cuda:{scene.info()['device']}")
+    _require_u32(out, words)
+    check(lib().vr_render(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
+                          f3(info.translation), int(info.scale), int(width), int(height), int(row_begin),
+                          int(row_end), c_void_p(out.data_ptr()), _stream_ptr(stream)), "vr_render")
+    return out
+
+
+def render_count(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
+                 info: VoxelSceneInfo, width: int, height: int, out: torch.Tensor, counter: torch.Tensor,
+                 row_begin: int = 0, row_end: int | None = None, stream=None) -> None:
+    """Instrumented render: adds the SURVEY 8(d) algorithmic bytes into counter (int64 cuda scalar)."""
+    row_end = height if row_end is None else row_end
+    _require_u32(out, (row_end - row_begin) * width)
+    if not counter.is_cuda or counter.dtype != torch.int64:
+        raise TypeError("counter must be a CUDA int64 tensor")
+    check(lib().vr_render_count(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
+                                f3(info.translation), int(info.scale), int(width), int(height), int(row_begin),
+                                int(row_end), c_void_p(out.data_ptr()), c_void_p(counter.data_ptr()),
+                                _stream_ptr(stream)), "vr_render_count")
+
+
+def band_buffer_words(width: int, height: int, band_rows: int, nranks: int) -> int:
+    return int(lib().vr_band_buffer_words(width, height, band_rows, nranks))
+
+
+def render_bands(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
+                 info: VoxelSceneInfo, width: int, height: int, band_rows: int, rank: int, nranks: int,
+                 out: torch.Tensor, stream=None) -> torch.Tensor:
+    """This rank's interleaved row bands (band b -> rank b % nranks), packed."""
+    _require_u32(out, band_buffer_words(width, height, band_rows, nranks))
+    check(lib().vr_render_bands(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
+                                f3(info.translation), int(info.scale), int(width), int(height), int(band_rows),
+                                int(rank), int(nranks), c_void_p(out.data_ptr()), _stream_ptr(stream)),
+          "vr_render_bands")
+    return out
+
+
+def pack_rgb8(words: torch.Tensor, stream=None) -> torch.Tensor:
+    """writeColorToFramebuffer (Renderer.cuh:1024-1031) on the device: words -> RGB8 bytes."""
+    rgb = torch.empty(words.numel() * 3, dtype=torch.uint8, device=words.device)
+    check(lib().vr_pack_rgb8(c_void_p(words.data_ptr()), c_void_p(rgb.data_ptr()), words.numel(),
+                             _stream_ptr(stream)), "vr_pack_rgb8")
+    return rgb
+
+
+@dataclass
+class RenderConfig:
+    """One BASELINE.json config."""
+    name: str
+    grid: int
+    p_region: float
+    p_cluster: float
+    p_voxel: float
+    seed: int
+    width: int
+    height: int
+    store: StorageType
+    algorithm: RayMarchAlgorithm
+    gpus: int = 1
+    notes: str = ""
+    scale: int = field(init=False)
+
+    def __post_init__(self):
+        self.scale = 3 * self.grid // 16        # eye at (6s,2s,6s): just outside the grid's x/z faces
+
+    def voxels(self):
+        return synth_scene(self.grid, self.p_region, self.p_cluster, self.p_voxel, self.seed)
+
+
+CONFIGS = {
+    "C1": RenderConfig("C1", 64, 1.0, 0.5, 0.10, 0x1, 256, 256, StorageType.HASH_TABLE, RayMarchAlgorithm.ORIGINAL,
+                       notes="scene.vox 64^3, hashtable+original (host-CPU plumbing config)"),
+    "C2": RenderConfig("C2", 256, 1.0, 0.30, 0.08, 0x256, 1920, 1080, StorageType.VOXEL_CLUSTER_STORE,
+                       RayMarchAlgorithm.ORIGINAL, notes="256^3 synthetic, vcs+original"),
+    "C3": RenderConfig("C3", 256, 1.0, 0.30, 0.08, 0x256, 1920, 1080, StorageType.VOXEL_CLUSTER_STORE,
+                       RayMarchAlgorithm.LONGEST_AXIS, notes="256^3 synthetic, vcs+longestaxis"),
+    "C4": RenderConfig("C4", 512, 1.0, 1.0, 0.15, 0x512, 1920, 1080, StorageType.HASH_TABLE,
+                       RayMarchAlgorithm.ORIGINAL, notes="512^3 dense, hashtable+original"),
+    "C5": RenderConfig("C5", 1024, 0.35, 0.05, 0.25, 0x1024, 3840, 2160, StorageType.VOXEL_CLUSTER_STORE,
+                       RayMarchAlgorithm.ORIGINAL, gpus=8, notes="1024^3 sparse, vcs+original, 8-GPU tiles"),
+}
