@@ -126,6 +126,29 @@ int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
 /* Number of uint32 words vr_render_bands writes per rank. */
 uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t nranks);
 
+/* Kernel implementations behind vr_render*: both produce identical pixels. */
+typedef enum {
+    VR_KERNEL_PERSISTENT = 0,   /* default: persistent state machine, one voxel probe per lane-iteration,
+                                   primary + shadow rays fused, global pixel queue (vr_persist.hip) */
+    VR_KERNEL_TILE = 1          /* one lane per pixel, one wave per 8x8 tile (vr_march.hip) */
+} vr_kernel;
+
+/* Full-control render (the other vr_render* calls are wrappers of this):
+ * rows [row_begin,row_end) of the frame cut into bands of band_rows rows,
+ * band b rendered when b % nranks == rank; out_dev gets this rank's bands
+ * packed as in vr_render_bands.  bytes_dev (optional, device uint64,
+ * caller-zeroed) accumulates the SURVEY.md 8(d) algorithmic bytes. */
+typedef struct {
+    uint32_t kernel;      /* vr_kernel */
+    uint32_t row_begin, row_end;
+    uint32_t band_rows;   /* 0 = one band covering [row_begin,row_end) */
+    uint32_t rank, nranks;
+    uint64_t* bytes_dev;
+} vr_render_opts;
+int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
+                 const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
+                 const vr_render_opts* opts, uint32_t* out_dev, void* stream);
+
 /* Same render as vr_render, plus the SURVEY.md 8(d) algorithmic byte count of
  * the launch accumulated into *bytes_dev (device uint64, caller-zeroed).
  * Instrumented variant for measurement; pixels are identical. */

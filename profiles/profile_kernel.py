@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Profiling driver: render one BASELINE config `--iters` times (kernel only,
+inputs resident), printing the HIP-event average per launch.  Run under
+rocprofv3 by profiles/run_rocprof.sh."""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import voxelraymarcher_amd as vr  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--config", default="C2")
+p.add_argument("--iters", type=int, default=20)
+p.add_argument("--no-shadows", action="store_true")
+p.add_argument("--algo", choices=["original", "longestaxis"], default=None)
+p.add_argument("--store", choices=["vcs", "hashtable"], default=None)
+p.add_argument("--kernel", choices=["persistent", "tile"], default="persistent")
+a = p.parse_args()
+kern = vr.Kernel.TILE if a.kernel == "tile" else vr.Kernel.PERSISTENT
+cfg = vr.CONFIGS[a.config]
+store = cfg.store if a.store is None else vr.parse_storage(a.store)
+algo = cfg.algorithm if a.algo is None else vr.parse_algorithm(a.algo)
+xyz, rgb = cfg.voxels()
+scene = vr.create_scene(xyz, rgb, store)
+W, H = cfg.width, cfg.height
+cam = vr.Camera.reference(W, H)
+lit = vr.setup_constant_values(use_shadows=not a.no_shadows)
+info = vr.VoxelSceneInfo((0, 0, 0), cfg.scale)
+out = torch.empty(W * H, dtype=torch.int32, device="cuda")
+s = torch.cuda.current_stream()
+vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, kernel=kern)
+torch.cuda.synchronize()
+ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
+for e0, e1 in ev:
+    e0.record(s)
+    vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, kernel=kern)
+    e1.record(s)
+torch.cuda.synchronize()
+ms = [e0.elapsed_time(e1) for e0, e1 in ev]
+print(f"{a.config} {a.kernel} {store.name} {algo.name} shadows={not a.no_shadows}: mean {np.mean(ms):.4f} ms "
+      f"min {np.min(ms):.4f} ms -> {W * H / np.mean(ms) / 1e3:.1f} Mrays/s", flush=True)

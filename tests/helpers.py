@@ -30,20 +30,21 @@ def oracle_lighting_from(lit) -> "oracle.OrLighting":
     return o
 
 
-def gpu_render(scene, algo, cam, lit, info, W, H, row_begin=0, row_end=None, count=False):
+def gpu_render(scene, algo, cam, lit, info, W, H, row_begin=0, row_end=None, count=False, kernel=None):
     import torch
 
     import voxelraymarcher_amd as vr
     row_end = H if row_end is None else row_end
+    kernel = vr.Kernel.PERSISTENT if kernel is None else kernel
     out = torch.full(((row_end - row_begin) * W,), -1, dtype=torch.int32, device="cuda")
     nbytes = None
     if count:
         ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
-        vr.render_count(scene, algo, cam, lit, info, W, H, out, ctr, row_begin, row_end)
+        vr.render_count(scene, algo, cam, lit, info, W, H, out, ctr, row_begin, row_end, kernel=kernel)
         torch.cuda.synchronize()
         nbytes = int(ctr.item())
     else:
-        vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, row_begin, row_end)
+        vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, row_begin, row_end, kernel=kernel)
         torch.cuda.synchronize()
     return out.cpu().numpy().view(np.uint32), nbytes
 

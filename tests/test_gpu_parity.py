@@ -15,23 +15,27 @@ vr = pytest.importorskip("voxelraymarcher_amd")
 
 STORES = [vr.StorageType.VOXEL_CLUSTER_STORE, vr.StorageType.HASH_TABLE]
 ALGOS = [vr.RayMarchAlgorithm.ORIGINAL, vr.RayMarchAlgorithm.LONGEST_AXIS]
+KERNELS = [vr.Kernel.PERSISTENT, vr.Kernel.TILE]
 
 
 def check_frame(xyz, rgb, store, algo, W, H, scale, cam=None, lit=None, translation=(0.0, 0.0, 0.0),
-                row_begin=0, row_end=None, count=True, oracle_scene=None, gpu_scene=None):
+                row_begin=0, row_end=None, count=True, oracle_scene=None, gpu_scene=None, kernels=KERNELS):
     row_end = H if row_end is None else row_end
     cam = cam or vr.Camera.reference(W, H)
     lit = lit or vr.setup_constant_values()
     info = vr.VoxelSceneInfo(translation, scale)
     scene = gpu_scene or vr.create_scene(xyz, rgb, store)
     ref = oracle_scene or oracle.Scene(xyz, rgb, int(store))
-    got, gbytes = gpu_render(scene, algo, cam, lit, info, W, H, row_begin, row_end, count=count)
     want, obytes = ref.render(int(algo), oracle_camera_from(cam), oracle_lighting_from(lit), W, H, scale,
                               translation, row_begin, row_end)
-    assert np.array_equal(got, want), diff_report(got, want, W, row_begin)
-    if count:
-        assert gbytes == obytes, f"algorithmic bytes: gpu {gbytes} != oracle {obytes}"
-    return got
+    for kernel in kernels:
+        got, gbytes = gpu_render(scene, algo, cam, lit, info, W, H, row_begin, row_end, count=count, kernel=kernel)
+        assert np.array_equal(got, want), f"{kernel.name}: " + diff_report(got, want, W, row_begin)
+        if count:
+            assert gbytes == obytes, f"{kernel.name}: algorithmic bytes: gpu {gbytes} != oracle {obytes}"
+        got2, _ = gpu_render(scene, algo, cam, lit, info, W, H, row_begin, row_end, count=False, kernel=kernel)
+        assert np.array_equal(got2, want), f"{kernel.name} (uncounted): " + diff_report(got2, want, W, row_begin)
+    return want
 
 
 @pytest.fixture(scope="module")

@@ -47,6 +47,14 @@ class VrSynthParams(ctypes.Structure):
                 ("seed", c_uint64)]
 
 
+VR_KERNEL_PERSISTENT, VR_KERNEL_TILE = 0, 1
+
+
+class VrRenderOpts(ctypes.Structure):
+    _fields_ = [("kernel", c_uint32), ("row_begin", c_uint32), ("row_end", c_uint32), ("band_rows", c_uint32),
+                ("rank", c_uint32), ("nranks", c_uint32), ("bytes_dev", c_void_p)]
+
+
 class VrError(RuntimeError):
     def __init__(self, code: int, where: str, msg: str):
         super().__init__(f"{where}: {ERRORS.get(code, code)}: {msg}")
@@ -67,6 +75,8 @@ SIGNATURES = {
     "vr_render_bands": (c_int, [c_void_p, c_int, POINTER(VrCamera), POINTER(VrLighting), POINTER(c_float),
                                 c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p, c_void_p]),
     "vr_band_buffer_words": (c_uint64, [c_uint32, c_uint32, c_uint32, c_uint32]),
+    "vr_render_ex": (c_int, [c_void_p, c_int, POINTER(VrCamera), POINTER(VrLighting), POINTER(c_float), c_uint32,
+                             c_uint32, c_uint32, POINTER(VrRenderOpts), c_void_p, c_void_p]),
     "vr_render_count": (c_int, [c_void_p, c_int, POINTER(VrCamera), POINTER(VrLighting), POINTER(c_float),
                                 c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p]),
     "vr_pack_rgb8": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
@@ -106,6 +116,6 @@ def f3(v) -> ctypes.Array:
     return (c_float * 3)(*[float(x) for x in v])
 
 
-__all__ = ["lib", "check", "VrCamera", "VrLighting", "VrSceneInfo", "VrSynthParams", "VrError", "SIGNATURES",
+__all__ = ["lib", "check", "VrCamera", "VrLighting", "VrRenderOpts", "VR_KERNEL_PERSISTENT", "VR_KERNEL_TILE", "VrSceneInfo", "VrSynthParams", "VrError", "SIGNATURES",
            "VR_STORE_VCS", "VR_STORE_HASHTABLE", "VR_ALGO_LONGESTAXIS", "VR_ALGO_ORIGINAL", "f3", "LIB_PATH",
            "c_uint8"]

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -350,10 +352,51 @@ int make_view(const vr_scene* s, const vr_camera* cam, const vr_lighting* lit, c
     return VR_OK;
 }
 
-int launch(const vr_scene* s, vr_algo algo, bool count, vr::KView& v, void* stream) {
+// Per-device ring of persistent-kernel queue slots (2 uint32 each, zeroed once;
+// every launch leaves its slot zeroed).  Launches in flight at the same time
+// (other streams) get different slots as long as fewer than kQueueSlots are
+// outstanding.
+constexpr uint32_t kQueueSlots = 1024;
+struct QueueRing {
+    std::mutex mu;
+    uint32_t* base[64] = {nullptr};
+    std::atomic<uint32_t> next{0};
+};
+QueueRing g_ring;
+
+int queue_slot(int dev, uint32_t** out) {
+    if (dev < 0 || dev >= 64) return fail(VR_E_INVALID, "device index too large");
+    if (!g_ring.base[dev]) {
+        std::lock_guard<std::mutex> lk(g_ring.mu);
+        if (!g_ring.base[dev]) {
+            void* p = nullptr;
+            hipError_t e = hipMalloc(&p, kQueueSlots * 2 * sizeof(uint32_t));
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(queue ring)");
+            e = hipMemset(p, 0, kQueueSlots * 2 * sizeof(uint32_t));
+            if (e != hipSuccess) return hip_fail(e, "hipMemset(queue ring)");
+            e = hipDeviceSynchronize();
+            if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+            g_ring.base[dev] = (uint32_t*)p;
+        }
+    }
+    *out = g_ring.base[dev] + 2 * (g_ring.next.fetch_add(1) % kQueueSlots);
+    return VR_OK;
+}
+
+int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void* stream) {
     if (algo != VR_ALGO_ORIGINAL && algo != VR_ALGO_LONGESTAXIS) return fail(VR_E_INVALID, "unknown algorithm");
+    if (v.local_rows == 0 || v.W == 0) return VR_OK;
     DeviceGuard dg(s->device);
-    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, (hipStream_t)stream);
+    const bool count = v.bytes != nullptr;
+    hipError_t e;
+    if (kernel == VR_KERNEL_TILE) {
+        e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, (hipStream_t)stream);
+    } else {
+        uint32_t* q = nullptr;
+        int rc = queue_slot(s->device, &q);
+        if (rc) return rc;
+        e = vr::launch_persist((int)s->store, (int)algo, count, kscene(s), v, q, (hipStream_t)stream);
+    }
     if (e != hipSuccess) return hip_fail(e, "ray-march launch");
     return VR_OK;
 }
@@ -459,20 +502,35 @@ void vr_scene_destroy(vr_scene* s) {
     free_scene(s);
 }
 
-int vr_render(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit, const float translation[3],
-              uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin, uint32_t row_end, uint32_t* out_dev,
-              void* stream) {
+int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
+                 const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
+                 const vr_render_opts* opts, uint32_t* out_dev, void* stream) {
     vr::KView v;
     int rc = make_view(s, cam, lit, translation, scale, width, height, v);
     if (rc) return rc;
-    if (row_begin > row_end || row_end > height) return fail(VR_E_INVALID, "bad row range");
+    if (!opts) return fail(VR_E_INVALID, "opts is NULL");
     if (!out_dev) return fail(VR_E_INVALID, "out_dev is NULL");
-    v.row0 = row_begin;
-    v.band_rows = std::max(1u, row_end - row_begin);
-    v.rank = 0; v.nranks = 1;
-    v.local_rows = row_end - row_begin;
+    if (opts->row_begin > opts->row_end || opts->row_end > height) return fail(VR_E_INVALID, "bad row range");
+    if (!opts->nranks || opts->rank >= opts->nranks) return fail(VR_E_INVALID, "bad band partition");
+    if (opts->kernel != VR_KERNEL_PERSISTENT && opts->kernel != VR_KERNEL_TILE) return fail(VR_E_INVALID, "unknown kernel");
+    const uint32_t rows = opts->row_end - opts->row_begin;
+    const uint32_t band = opts->band_rows ? opts->band_rows : std::max(1u, rows);
+    v.row0 = opts->row_begin;
+    v.row_limit = opts->row_end;
+    v.band_rows = band;
+    v.rank = opts->rank;
+    v.nranks = opts->nranks;
+    v.local_rows = (uint32_t)(vr_band_buffer_words(width, rows, band, opts->nranks) / width);
     v.out = out_dev;
-    return launch(s, algo, false, v, stream);
+    v.bytes = (unsigned long long*)opts->bytes_dev;
+    return launch(s, algo, opts->kernel, v, stream);
+}
+
+int vr_render(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit, const float translation[3],
+              uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin, uint32_t row_end, uint32_t* out_dev,
+              void* stream) {
+    vr_render_opts o{VR_KERNEL_PERSISTENT, row_begin, row_end, 0, 0, 1, nullptr};
+    return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
 uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t nranks) {
@@ -485,36 +543,17 @@ uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_row
 int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t band_rows,
                     uint32_t rank, uint32_t nranks, uint32_t* out_dev, void* stream) {
-    vr::KView v;
-    int rc = make_view(s, cam, lit, translation, scale, width, height, v);
-    if (rc) return rc;
-    if (!band_rows || !nranks || rank >= nranks) return fail(VR_E_INVALID, "bad band partition");
-    if (!out_dev) return fail(VR_E_INVALID, "out_dev is NULL");
-    uint64_t words = vr_band_buffer_words(width, height, band_rows, nranks);
-    v.row0 = 0;
-    v.band_rows = band_rows;
-    v.rank = rank;
-    v.nranks = nranks;
-    v.local_rows = (uint32_t)(words / width);
-    v.out = out_dev;
-    return launch(s, algo, false, v, stream);
+    if (!band_rows) return fail(VR_E_INVALID, "band_rows must be > 0");
+    vr_render_opts o{VR_KERNEL_PERSISTENT, 0, height, band_rows, rank, nranks, nullptr};
+    return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
 int vr_render_count(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin,
                     uint32_t row_end, uint32_t* out_dev, uint64_t* bytes_dev, void* stream) {
-    vr::KView v;
-    int rc = make_view(s, cam, lit, translation, scale, width, height, v);
-    if (rc) return rc;
-    if (row_begin > row_end || row_end > height) return fail(VR_E_INVALID, "bad row range");
-    if (!out_dev || !bytes_dev) return fail(VR_E_INVALID, "NULL device buffer");
-    v.row0 = row_begin;
-    v.band_rows = std::max(1u, row_end - row_begin);
-    v.rank = 0; v.nranks = 1;
-    v.local_rows = row_end - row_begin;
-    v.out = out_dev;
-    v.bytes = (unsigned long long*)bytes_dev;
-    return launch(s, algo, true, v, stream);
+    if (!bytes_dev) return fail(VR_E_INVALID, "bytes_dev is NULL");
+    vr_render_opts o{VR_KERNEL_PERSISTENT, row_begin, row_end, 0, 0, 1, bytes_dev};
+    return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
 int vr_pack_rgb8(const uint32_t* words_dev, uint8_t* rgb_dev, uint64_t n_pixels, void* stream) {

@@ -33,7 +33,8 @@ struct KScene {
 
 // Per-launch view: camera, lighting, scene transform and the row mapping.
 // Local row l of the output maps to frame row
-//   row0 + ((l / band_rows) * nranks + rank) * band_rows + (l % band_rows).
+//   y = row0 + ((l / band_rows) * nranks + rank) * band_rows + (l % band_rows);
+// rows with y >= row_limit (<= H) are written as 0.
 struct KView {
     float llc[3], hor[3], ver[3], org[3];
     float L[3], LC[3], LP[3];
@@ -41,7 +42,7 @@ struct KView {
     float scale_f;
     int32_t use_point_light, use_shadows;
     uint32_t W, H;
-    uint32_t row0, band_rows, rank, nranks, local_rows;
+    uint32_t row0, band_rows, rank, nranks, local_rows, row_limit;
     uint32_t* out;
     unsigned long long* bytes;
 };
@@ -49,6 +50,10 @@ struct KView {
 // Launch one render (defined in vr_march.hip).
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,
                         hipStream_t stream);
+// Persistent state-machine kernel (vr_persist.hip); `queue` = 2 zeroed uint32
+// words private to this launch (the kernel leaves them zeroed on exit).
+hipError_t launch_persist(int store, int algo, bool count, const KScene& s, const KView& v, uint32_t* queue,
+                          hipStream_t stream);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);
 
 }  // namespace vr

@@ -205,34 +205,57 @@ def _require_u32(out: torch.Tensor, words: int) -> None:
         raise ValueError(f"out must be contiguous with >= {words} elements")
 
 
+class Kernel(enum.IntEnum):
+    """vr_kernel: which HIP implementation renders (identical pixels)."""
+    PERSISTENT = _capi.VR_KERNEL_PERSISTENT
+    TILE = _capi.VR_KERNEL_TILE
+
+
+def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
+              info: VoxelSceneInfo, width: int, height: int, out: torch.Tensor, row_begin: int = 0,
+              row_end: int | None = None, band_rows: int = 0, rank: int = 0, nranks: int = 1,
+              counter: torch.Tensor | None = None, kernel: Kernel = Kernel.PERSISTENT, stream=None) -> torch.Tensor:
+    """vr_render_ex: rows [row_begin,row_end), bands of band_rows (0 = one band) dealt to nranks ranks."""
+    row_end = height if row_end is None else row_end
+    rows = row_end - row_begin
+    words = band_buffer_words(width, rows, band_rows or max(1, rows), nranks)
+    _require_u32(out, words)
+    if counter is not None and (not counter.is_cuda or counter.dtype != torch.int64):
+        raise TypeError("counter must be a CUDA int64 tensor")
+    opts = _capi.VrRenderOpts(int(kernel), int(row_begin), int(row_end), int(band_rows), int(rank), int(nranks),
+                              c_void_p(counter.data_ptr()) if counter is not None else None)
+    check(lib().vr_render_ex(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
+                             f3(info.translation), int(info.scale), int(width), int(height), ctypes.byref(opts),
+                             c_void_p(out.data_ptr()), _stream_ptr(stream)), "vr_render_ex")
+    return out
+
+
 def run_raymarching_kernel(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera,
                            lighting: _capi.VrLighting, info: VoxelSceneInfo, width: int, height: int,
                            out: torch.Tensor | None = None, row_begin: int = 0, row_end: int | None = None,
-                           stream=None) -> torch.Tensor:
+                           stream=None, kernel: Kernel = Kernel.PERSISTENT) -> torch.Tensor:
     """Launch the ray march for rows [row_begin,row_end) (Main.cu:105-163); asynchronous."""
     row_end = height if row_end is None else row_end
     words = (row_end - row_begin) * width
     if out is None:
         out = torch.empty(words, dtype=torch.int32, device=f"cuda:{scene.info()['device']}")
-    _require_u32(out, words)
-    check(lib().vr_render(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
-                          f3(info.translation), int(info.scale), int(width), int(height), int(row_begin),
-                          int(row_end), c_void_p(out.data_ptr()), _stream_ptr(stream)), "vr_render")
-    return out
+    if kernel == Kernel.PERSISTENT:
+        _require_u32(out, words)
+        check(lib().vr_render(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
+                              f3(info.translation), int(info.scale), int(width), int(height), int(row_begin),
+                              int(row_end), c_void_p(out.data_ptr()), _stream_ptr(stream)), "vr_render")
+        return out
+    return render_ex(scene, algorithm, camera, lighting, info, width, height, out, row_begin, row_end,
+                     kernel=kernel, stream=stream)
 
 
 def render_count(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
                  info: VoxelSceneInfo, width: int, height: int, out: torch.Tensor, counter: torch.Tensor,
-                 row_begin: int = 0, row_end: int | None = None, stream=None) -> None:
+                 row_begin: int = 0, row_end: int | None = None, stream=None,
+                 kernel: Kernel = Kernel.PERSISTENT) -> None:
     """Instrumented render: adds the SURVEY 8(d) algorithmic bytes into counter (int64 cuda scalar)."""
-    row_end = height if row_end is None else row_end
-    _require_u32(out, (row_end - row_begin) * width)
-    if not counter.is_cuda or counter.dtype != torch.int64:
-        raise TypeError("counter must be a CUDA int64 tensor")
-    check(lib().vr_render_count(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
-                                f3(info.translation), int(info.scale), int(width), int(height), int(row_begin),
-                                int(row_end), c_void_p(out.data_ptr()), c_void_p(counter.data_ptr()),
-                                _stream_ptr(stream)), "vr_render_count")
+    render_ex(scene, algorithm, camera, lighting, info, width, height, out, row_begin, row_end,
+              counter=counter, kernel=kernel, stream=stream)
 
 
 def band_buffer_words(width: int, height: int, band_rows: int, nranks: int) -> int:
