@@ -126,11 +126,12 @@ int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
 /* Number of uint32 words vr_render_bands writes per rank. */
 uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t nranks);
 
-/* Kernel implementations behind vr_render*: both produce identical pixels. */
+/* Kernel implementations behind vr_render*: all produce identical pixels. */
 typedef enum {
-    VR_KERNEL_PERSISTENT = 0,   /* default: persistent state machine, one voxel probe per lane-iteration,
-                                   primary + shadow rays fused, global pixel queue (vr_persist.hip) */
-    VR_KERNEL_TILE = 1          /* one lane per pixel, one wave per 8x8 tile (vr_march.hip) */
+    VR_KERNEL_AUTO = 0,         /* the fastest measured for the (store, algorithm) pair */
+    VR_KERNEL_TILE = 1,         /* one lane per pixel, one wave per 8x8 tile (vr_march.hip) */
+    VR_KERNEL_PERSISTENT = 2    /* persistent state machine: one voxel probe per lane-iteration,
+                                   primary + shadow rays fused, tile queue (vr_persist.hip) */
 } vr_kernel;
 
 /* Full-control render (the other vr_render* calls are wrappers of this):

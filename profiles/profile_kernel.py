@@ -18,9 +18,9 @@ p.add_argument("--iters", type=int, default=20)
 p.add_argument("--no-shadows", action="store_true")
 p.add_argument("--algo", choices=["original", "longestaxis"], default=None)
 p.add_argument("--store", choices=["vcs", "hashtable"], default=None)
-p.add_argument("--kernel", choices=["persistent", "tile"], default="persistent")
+p.add_argument("--kernel", choices=["auto", "persistent", "tile"], default="auto")
 a = p.parse_args()
-kern = vr.Kernel.TILE if a.kernel == "tile" else vr.Kernel.PERSISTENT
+kern = {"auto": vr.Kernel.AUTO, "tile": vr.Kernel.TILE, "persistent": vr.Kernel.PERSISTENT}[a.kernel]
 cfg = vr.CONFIGS[a.config]
 store = cfg.store if a.store is None else vr.parse_storage(a.store)
 algo = cfg.algorithm if a.algo is None else vr.parse_algorithm(a.algo)

@@ -35,7 +35,7 @@ def gpu_render(scene, algo, cam, lit, info, W, H, row_begin=0, row_end=None, cou
 
     import voxelraymarcher_amd as vr
     row_end = H if row_end is None else row_end
-    kernel = vr.Kernel.PERSISTENT if kernel is None else kernel
+    kernel = vr.Kernel.AUTO if kernel is None else kernel
     out = torch.full(((row_end - row_begin) * W,), -1, dtype=torch.int32, device="cuda")
     nbytes = None
     if count:

@@ -1,0 +1,466 @@
+"""Second, independent restatement of the reference traversal in pure Python
+with numpy.float32 scalars (TEST INFRASTRUCTURE ONLY).
+
+Written separately from oracle/vr_oracle.c, from the reference source text
+(paths relative to /root/reference/VoxelRaymarcher/src), to catch
+transcription errors in the C oracle: the tests run both on the same rays and
+demand identical packed pixels.  Slow -- meant for a few hundred rays.
+
+Storage is a plain dict per region {local key: colour} plus the set of
+non-empty 8^3 clusters; lookups return the same values as VoxelClusterStore /
+CuckooHashTable (any correct structure does), and the VCS existence test is
+the cluster set (VoxelClusterStore.cuh:93-99).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+F = np.float32
+EPS = F(0.0001)                      # VoxelFunctions.cuh:19
+EMPTY = 1 << 30                      # :20-21
+CONTINUE = EMPTY + 2                 # :23
+INF = F(np.inf)
+BLOCK = 64
+
+
+def f2i(v) -> int:
+    """static_cast<int32_t>(float) on the device: truncate, saturate, NaN -> 0."""
+    v = float(v)
+    if math.isnan(v):
+        return 0
+    if v >= 2147483648.0:
+        return 2147483647
+    if v <= -2147483648.0:
+        return -2147483648
+    return int(v)
+
+
+def wrap32(v: int) -> int:
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v & 0x80000000 else v
+
+
+def u32(v: int) -> int:
+    return v & 0xFFFFFFFF
+
+
+class V:
+    """Vector3f with the reference's operator order (Vector3.cuh)."""
+    __slots__ = ("x",)
+
+    def __init__(self, a, b, c):
+        self.x = [F(a), F(b), F(c)]
+
+    def __getitem__(self, i):
+        return self.x[i]
+
+    def __add__(self, o):
+        return V(self.x[0] + o.x[0], self.x[1] + o.x[1], self.x[2] + o.x[2])
+
+    def __sub__(self, o):
+        return V(self.x[0] - o.x[0], self.x[1] - o.x[1], self.x[2] - o.x[2])
+
+    def mul(self, o):
+        return V(self.x[0] * o.x[0], self.x[1] * o.x[1], self.x[2] * o.x[2])
+
+    def scale(self, t):                  # t * v[i] (Vector3.cuh:130-133, 142-145)
+        t = F(t)
+        return V(t * self.x[0], t * self.x[1], t * self.x[2])
+
+    def length(self):                    # :79
+        return F(np.sqrt(self.x[0] * self.x[0] + self.x[1] * self.x[1] + self.x[2] * self.x[2]))
+
+    def unit(self):                      # :162-165 -> v / length (:136-139)
+        n = self.length()
+        return V(self.x[0] / n, self.x[1] / n, self.x[2] / n)
+
+    def copy(self):
+        return V(*self.x)
+
+
+def dot(a, b):
+    return a.x[0] * b.x[0] + a.x[1] * b.x[1] + a.x[2] * b.x[2]
+
+
+def cross(a, b):
+    return V(a[1] * b[2] - a[2] * b[1], -(a[0] * b[2] - a[2] * b[0]), a[0] * b[1] - a[1] * b[0])
+
+
+def fmin3(a, b, c):
+    return np.fmin(a, np.fmin(b, c))
+
+
+class Scene:
+    def __init__(self, xyz, rgb, store: int):
+        """VoxelSceneCPU::insertVoxel (VoxelSceneCPU.cuh:16-46) over the voxels."""
+        self.store = store
+        self.regions = {}
+        mn = mx = 0
+        for (x, y, z), c in zip(np.asarray(xyz).tolist(), np.asarray(rgb).tolist()):
+            r = tuple(f2i(np.floor(F(v) / F(64))) for v in (x, y, z))
+            loc = tuple(((v % 64) + 64) % 64 for v in (x, y, z))   # Python % is already non-negative
+            mn = min(mn, *r)
+            mx = max(mx, *r)
+            key = (loc[0] << 20) | (loc[1] << 10) | loc[2]
+            self.regions.setdefault(r, {})[key] = int(c)
+        self.min = mn
+        self.D = mx - mn + 1
+        self.clusters = {r: {((k >> 20) // 8, ((k >> 10) & 0x3FF) // 8, (k & 0x3FF) // 8) for k in d}
+                         for r, d in self.regions.items()}
+
+
+class Lighting:
+    def __init__(self, shadows=True, point=False, pos=(10.0, 10.0, -10.0)):
+        self.L = V(1.0, 1.0, 1.0).unit()      # Main.cu:28
+        self.LC = V(1.0, 1.0, 1.0)
+        self.LP = V(*pos)
+        self.shadows = shadows
+        self.point = point
+
+
+class Walk:
+    """One pixel's traversal (Renderer.cuh)."""
+
+    def __init__(self, scene: Scene, lit: Lighting, translation):
+        self.s = scene
+        self.lit = lit
+        self.tr = V(*translation)
+        self.iters = 0
+        self.aborted = False
+
+    def tick(self):
+        if self.aborted:
+            return False
+        self.iters += 1
+        if self.iters > 65536:
+            self.aborted = True
+            return False
+        return True
+
+    # VoxelScene (Renderer.cuh:20-45)
+    def in_scene(self, r):
+        return all(u32(v - self.s.min) < self.s.D for v in r)
+
+    def region(self, r):
+        return tuple(r) if tuple(r) in self.s.regions else None
+
+    # StorageStructure adapters (StorageStructure.cuh:24-52)
+    def exists(self, reg, x, y, z):
+        if self.s.store == 1:
+            return True
+        ux, uy, uz = u32(x), u32(y), u32(z)
+        cid = (((ux // 8) << 6) | ((uy // 8) << 3) | (uz // 8)) & 0xFFFF
+        if cid >= 0x8000 or cid >= 512:            # `short` id outside the directory
+            return False
+        return (cid >> 6, (cid >> 3) & 7, cid & 7) in self.s.clusters[reg]
+
+    def lookup(self, reg, x, y, z):
+        key = u32((u32(x) << 20) | (u32(y) << 10) | u32(z))
+        return self.s.regions[reg].get(key, EMPTY)
+
+    # lighting (Renderer.cuh:57-86, 249-258; VoxelFunctions.cuh:69-83)
+    @staticmethod
+    def to_vec(c):
+        return V(F(c >> 16) / F(255), F((c >> 8) & 0xFF) / F(255), F(c & 0xFF) / F(255))
+
+    @staticmethod
+    def to_int(v):
+        ch = [0 if (math.isnan(float(e)) or float(e) <= 0) else int(float(e)) for e in (v[0] * F(255), v[1] * F(255), v[2] * F(255))]
+        return (ch[0] << 16) | (ch[1] << 8) | ch[2]
+
+    def lighting(self, color, n, rwp, ro):
+        if self.lit.point:
+            hp = rwp + ro
+            p2l = self.lit.LP - hp
+            dist = p2l.length()
+            ld = p2l.unit()
+            att = F(1) / (F(1.0) + F(0.045) * dist + F(0.0075) * (dist * dist))
+            diff = np.fmax(dot(n, ld), F(0))
+            diffuse = self.lit.LC.scale(diff)
+            return self.to_int(diffuse.scale(att).mul(self.to_vec(color)))
+        diff = np.fmax(dot(n, self.lit.L), F(0))
+        diffuse = self.lit.LC.scale(diff)
+        return self.to_int(self.to_vec(color).mul(diffuse))
+
+    @staticmethod
+    def normal(tX, tY, tZ, tMin, d):        # Renderer.cuh:237-247
+        if tX == tMin:
+            return V(np.copysign(F(1), -d[0]), 0, 0)
+        if tY == tMin:
+            return V(0, np.copysign(F(1), -d[1]), 0)
+        return V(0, 0, np.copysign(F(1), -d[2]))
+
+    @staticmethod
+    def nxt(pos, x):                         # Renderer.cuh:47-55
+        return F(np.ceil(x)) + EPS if pos else F(np.floor(x)) - EPS
+
+    @staticmethod
+    def in_region(o):
+        return all(F(0) <= o[i] < F(BLOCK) for i in range(3))
+
+    @staticmethod
+    def grid_in(a, b, c):
+        return all(u32(v) < BLOCK for v in (a, b, c))
+
+    @staticmethod
+    def div(a, b, guard=False):
+        a, b = F(a), F(b)
+        if guard and b == 0:
+            return INF
+        with np.errstate(divide="ignore", invalid="ignore"):
+            return F(a / b)
+
+    def shift_region(self, cr, o):
+        d = [f2i(np.floor(o[i] / F(BLOCK))) for i in range(3)]
+        for i in range(3):
+            cr[i] = wrap32(cr[i] + d[i])
+        return (o - V(wrap32(d[0] * BLOCK), wrap32(d[1] * BLOCK), wrap32(d[2] * BLOCK))).scale(1.0)
+
+    # rayMarchVoxelGrid (:260-336) / shadowRayMarchVoxelGrid (:100-172)
+    def grid(self, ray, reg, rwp, cr, shadow):
+        o, d = ray[0], ray[1]
+        pos = [d[i] > 0 for i in range(3)]
+        t = [self.div(self.nxt(pos[i], o[i]) - o[i], d[i], shadow) for i in range(3)]
+        tMin = fmin3(*t)
+        ray[0] = o + d.scale(tMin + EPS)
+        while self.in_region(ray[0]):
+            if not self.tick():
+                return EMPTY
+            o = ray[0]
+            vx, vy, vz = (f2i(o[i]) for i in range(3))
+            if not self.exists(reg, vx, vy, vz):
+                nb = []
+                for i, vv in enumerate((vx, vy, vz)):
+                    q = int(vv / 8)      # C truncating division
+                    nb.append((q + 1) * 8 if pos[i] else q * 8)
+                st = [self.div(F(nb[i]) - o[i], d[i], shadow) for i in range(3)]
+                ray[0] = o + d.scale(fmin3(*st) + EPS)
+                continue
+            col = self.lookup(reg, vx, vy, vz)
+            if col != EMPTY:
+                if shadow:
+                    return col
+                lit = self.lighting(col, self.normal(t[0], t[1], t[2], tMin, d), rwp, o)
+                return lit * (0 if self.shadow_scene([o.copy(), self.lit.L], list(cr), False) else 1)
+            t = [self.div(self.nxt(pos[i], o[i]) - o[i], d[i], shadow) for i in range(3)]
+            tMin = fmin3(*t)
+            ray[0] = o + d.scale(tMin + EPS)
+        return EMPTY
+
+    def null_skip(self, lr, cr, guard):       # :386-409 / :187-210
+        o, d = lr[0], lr[1]
+        n = [F(BLOCK) + EPS if d[i] > 0 else F(0) - EPS for i in range(3)]
+        t = [self.div(n[i] - o[i], d[i], guard) for i in range(3)]
+        lr[0] = self.shift_region(cr, o + d.scale(fmin3(*t)))
+
+    # isInShadowOriginalRayMarch (:174-235) / ...LongestAxis (:633-694)
+    def shadow_scene(self, lr, cr, longest):
+        if not self.lit.shadows:
+            return False
+        while self.in_scene(cr):
+            if not self.tick():
+                return False
+            reg = self.region(cr)
+            while reg is None:
+                if not self.tick():
+                    return False
+                self.null_skip(lr, cr, not longest)
+                if not self.in_scene(cr):
+                    return False
+                reg = self.region(cr)
+            col = self.grid_la(lr, reg, V(0, 0, 0), cr, True) if longest else self.grid(lr, reg, None, cr, True)
+            if self.aborted:
+                return False
+            if col != EMPTY:
+                return True
+            lr[0] = self.shift_region(cr, lr[0])
+        return False
+
+    # rayMarchVoxelGridLongestAxis (:760-915) / shadow twin (:495-631)
+    def grid_la(self, orig, reg, rwp, cr, shadow):
+        od = orig[1]
+        a = [abs(od[i]) for i in range(3)]
+        if a[0] > a[1] and a[0] > a[2]:
+            L, (M, S), k = 0, ((1, 2) if a[1] > a[2] else (2, 1)), F(1) / a[0]
+        elif a[1] > a[2]:
+            L, (M, S), k = 1, ((0, 2) if a[0] > a[2] else (2, 0)), F(1) / a[1]
+        else:
+            L, (M, S), k = 2, ((0, 1) if a[0] > a[1] else (1, 0)), F(1) / a[2]
+        ds = od.scale(k)
+        old = orig[0].copy()
+        g = [f2i(orig[0][i]) for i in range(3)]
+        ad = [0, 0, 0]
+        ad[L] = -1 if od[L] < 0 else 1
+        if ad[L] > 0:
+            t = (F(g[L]) + EPS + F(1) - orig[0][L]) / F(ad[L])
+        else:
+            t = (F(g[L]) - EPS - orig[0][L]) / F(ad[L])
+        ray = old + ds.scale(t)
+        ad[M] = wrap32(f2i(ray[M]) - g[M])
+        ad[S] = wrap32(f2i(ray[S]) - g[S])
+        floor_mid = ds[M] < 0
+        st = {"old": old, "ray": ray}
+
+        def hit(col, axis, loc):
+            if shadow:
+                return col
+            n = [F(0)] * 3
+            n[axis] = np.copysign(F(1), -ds[axis])
+            lit = self.lighting(col, V(*n), rwp, loc)
+            return lit * (0 if self.shadow_scene([loc.copy(), self.lit.L], list(cr), True) else 1)
+
+        def jump():                          # performVoxelSpaceJump (:696-751) / (:441-492)
+            tX = tY = tZ = tMin = F(0)
+            while not self.exists(reg, *g):
+                if not self.tick():
+                    return EMPTY
+                o = st["old"]
+                nb = []
+                for i in range(3):
+                    q = int(g[i] / 8)
+                    nb.append((q + 1) * 8 if ds[i] > 0 else q * 8)
+                tX, tY, tZ = (self.div(F(nb[i]) - o[i], ds[i]) for i in range(3))
+                tMin = fmin3(tX, tY, tZ) + EPS
+                st["old"] = o + ds.scale(tMin)
+                for i in range(3):
+                    g[i] = f2i(np.floor(st["old"][i]))
+                if not self.grid_in(*g):
+                    orig[0] = st["old"].copy()
+                    return EMPTY
+            col = self.lookup(reg, *g)
+            if col != EMPTY:
+                if shadow:
+                    return col
+                lit = self.lighting(col, self.normal(tX, tY, tZ, tMin, ds), rwp, st["old"])
+                return lit * (0 if self.shadow_scene([st["old"].copy(), self.lit.L], list(cr), True) else 1)
+            o = st["old"]
+            if ds[L] > 0:
+                tn = (F(np.ceil(o[L])) - o[L]) / ds[L]
+            else:
+                tn = (F(np.floor(o[L])) - o[L]) / ds[L]
+            st["ray"] = o + ds.scale(tn + EPS)
+            ad[M] = wrap32(f2i(st["ray"][M]) - g[M])
+            ad[S] = wrap32(f2i(st["ray"][S]) - g[S])
+            return CONTINUE
+
+        def step(axis, long_axis):
+            """-> ('ret', value) | ('cont',) | None"""
+            g[axis] = wrap32(g[axis] + ad[axis])
+            if not self.exists(reg, *g):
+                r = jump()
+                if self.aborted:
+                    return ("ret", EMPTY)
+                return ("ret", r) if r != CONTINUE else ("cont",)
+            col = self.lookup(reg, *g)
+            if col != EMPTY:
+                if long_axis:
+                    loc = st["ray"]
+                else:                        # getLocalHitLocation (:753-758)
+                    o = st["old"]
+                    if ds[axis] > 0:
+                        tt = (F(np.ceil(o[axis])) - o[axis]) / ds[axis]
+                    else:
+                        tt = (F(np.floor(o[axis])) - o[axis]) / ds[axis]
+                    loc = o + ds.scale(tt)
+                return ("ret", hit(col, axis, loc))
+            return None
+
+        while self.grid_in(wrap32(g[L] + ad[L]), wrap32(g[M] + ad[M]), wrap32(g[S] + ad[S])):
+            if not self.tick():
+                return EMPTY
+            if ad[S] != 0 and ad[M] != 0:
+                om = st["old"][M]
+                t1 = ((F(np.floor(om)) if floor_mid else F(np.ceil(om))) - om) / ds[M]
+                sp = st["old"][S] + ds[S] * t1
+                sd = wrap32(f2i(np.floor(sp)) - g[S])
+                order = [S, M] if sd != 0 else [M, S]
+            elif ad[M] != 0:
+                order = [M]
+            elif ad[S] != 0:
+                order = [S]
+            else:
+                order = []
+            res = None
+            for axis in order + [L]:
+                res = step(axis, axis == L)
+                if res is not None:
+                    break
+            if res is not None:
+                if res[0] == "ret":
+                    return res[1]
+                continue
+            st["old"] = st["ray"]
+            st["ray"] = st["ray"] + ds
+            ad[M] = wrap32(f2i(st["ray"][M]) - g[M])
+            ad[S] = wrap32(f2i(st["ray"][S]) - g[S])
+        orig[0] = st["old"].copy()
+        return self.grid(orig, reg, rwp, cr, shadow)
+
+    # rayMarchVoxelScene (:338-434) / rayMarchVoxelSceneLongestAxis (:917-1010)
+    def scene(self, world_o, world_d, scale, longest):
+        so = (world_o - self.tr).scale(F(scale))
+        d = world_d
+        cr = [f2i(np.floor(so[i] / F(BLOCK))) for i in range(3)]
+        while not self.in_scene(cr):
+            if not self.tick():
+                return 0
+            hi = wrap32(self.s.D + self.s.min)
+            lo = self.s.min
+            t = []
+            for i in range(3):
+                n = hi if d[i] < 0 else lo
+                tv = self.div(F(wrap32(n * BLOCK)) - so[i], d[i])
+                t.append(INF if tv <= 0 else tv)
+            tMin = fmin3(*t)
+            if tMin == INF:
+                return 0
+            so = so + d.scale(tMin + EPS)
+            cr = [f2i(np.floor(so[i] / F(BLOCK))) for i in range(3)]
+        lr = [(so - V(wrap32(cr[0] * BLOCK), wrap32(cr[1] * BLOCK), wrap32(cr[2] * BLOCK))).scale(1.0), d]
+        while self.in_scene(cr):
+            if not self.tick():
+                return 0
+            reg = self.region(cr)
+            while reg is None:
+                if not self.tick():
+                    return 0
+                self.null_skip(lr, cr, False)
+                if not self.in_scene(cr):
+                    return 0
+                reg = self.region(cr)
+            rwp = self.tr + V(wrap32(cr[0] * BLOCK), wrap32(cr[1] * BLOCK), wrap32(cr[2] * BLOCK))
+            col = self.grid_la(lr, reg, rwp, cr, False) if longest else self.grid(lr, reg, rwp, cr, False)
+            if self.aborted:
+                return 0
+            if col != EMPTY:
+                return col
+            lr[0] = self.shift_region(cr, lr[0])
+        return 0
+
+
+def camera(eye, at, up, fov, aspect):
+    """Camera::Camera (Camera.cuh:11-23) -> (origin, llc, horizontal, vertical)."""
+    PI = F(3.141592)
+    hh = F(math.tan(float((F(fov) * PI / F(180)) / F(2))))
+    # tanf: take the float32 rounding of the double tan of the float32 argument
+    hw = hh * F(aspect)
+    o = V(*eye)
+    w = (V(*at) - o).unit()
+    u = cross(w, V(*up)).unit()
+    v = cross(u, w)
+    llc = ((o - u.scale(hw)) - v.scale(hh)) + w
+    return o, llc, u.scale(F(2) * hw), v.scale(F(2) * hh)
+
+
+def render_pixel(scene, lit, cam_fields, W, H, x, y, scale, longest, translation=(0.0, 0.0, 0.0)):
+    """calculateWorldRay + kernel body (Renderer.cuh:1013-1063). cam_fields: (origin, llc, hor, ver) V's."""
+    org, llc, hor, ver = cam_fields
+    u = (F(x) + F(0.5)) / F(W)
+    v = (F(u32(H - y)) + F(0.5)) / F(H)
+    ro = (llc + hor.scale(u)) + ver.scale(v)
+    rd = (ro - org).unit()
+    w = Walk(scene, lit, translation)
+    col = w.scene(ro, rd, scale, longest)
+    return 0 if w.aborted else col

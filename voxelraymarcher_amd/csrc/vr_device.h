@@ -46,17 +46,20 @@ __device__ __forceinline__ void setf(f3& v, uint32_t a, float val) {
     v.z = a == 2 ? val : v.z;
 }
 
-// static_cast<int32_t>(float) with CUDA device semantics (cvt.rzi.s32.f32).
+// static_cast<int32_t>(float) / static_cast<uint32_t>(float) with the CUDA
+// device semantics (cvt.rzi.s32.f32 / cvt.rzi.u32.f32: truncate, saturate,
+// NaN -> 0).  v_cvt_i32_f32 / v_cvt_u32_f32 implement exactly that on CDNA;
+// emitting them directly keeps the conversion one branch-free instruction
+// (a C cast is UB out of range and hipcc guards it with control flow).
 __device__ __forceinline__ int32_t f2i(float f) {
-    if (f != f) return 0;
-    if (f >= 2147483648.0f) return INT32_MAX;
-    if (f <= -2147483648.0f) return INT32_MIN;
-    return (int32_t)f;
+    int32_t r;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
+    return r;
 }
 __device__ __forceinline__ uint32_t f2u(float f) {
-    if (f != f || f <= 0.0f) return 0u;
-    if (f >= 4294967296.0f) return 0xFFFFFFFFu;
-    return (uint32_t)f;
+    uint32_t r;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(f));
+    return r;
 }
 
 // CuckooHashTable::hashFunc1 / hashFunc2 (CuckooHashTable.cuh:181-202),

@@ -352,11 +352,11 @@ int make_view(const vr_scene* s, const vr_camera* cam, const vr_lighting* lit, c
     return VR_OK;
 }
 
-// Per-device ring of persistent-kernel queue slots (2 uint32 each, zeroed once;
-// every launch leaves its slot zeroed).  Launches in flight at the same time
-// (other streams) get different slots as long as fewer than kQueueSlots are
-// outstanding.
-constexpr uint32_t kQueueSlots = 1024;
+// Per-device ring of persistent-kernel queue slots (vr::kQueueWords uint32
+// each, zeroed on the launch stream before every launch).  Launches in flight
+// at the same time (other streams) get different slots as long as fewer than
+// kQueueSlots are outstanding.
+constexpr uint32_t kQueueSlots = 256;
 struct QueueRing {
     std::mutex mu;
     uint32_t* base[64] = {nullptr};
@@ -370,16 +370,16 @@ int queue_slot(int dev, uint32_t** out) {
         std::lock_guard<std::mutex> lk(g_ring.mu);
         if (!g_ring.base[dev]) {
             void* p = nullptr;
-            hipError_t e = hipMalloc(&p, kQueueSlots * 2 * sizeof(uint32_t));
+            hipError_t e = hipMalloc(&p, (size_t)kQueueSlots * vr::kQueueWords * sizeof(uint32_t));
             if (e != hipSuccess) return hip_fail(e, "hipMalloc(queue ring)");
-            e = hipMemset(p, 0, kQueueSlots * 2 * sizeof(uint32_t));
+            e = hipMemset(p, 0, (size_t)kQueueSlots * vr::kQueueWords * sizeof(uint32_t));
             if (e != hipSuccess) return hip_fail(e, "hipMemset(queue ring)");
             e = hipDeviceSynchronize();
             if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
             g_ring.base[dev] = (uint32_t*)p;
         }
     }
-    *out = g_ring.base[dev] + 2 * (g_ring.next.fetch_add(1) % kQueueSlots);
+    *out = g_ring.base[dev] + (size_t)vr::kQueueWords * (g_ring.next.fetch_add(1) % kQueueSlots);
     return VR_OK;
 }
 
@@ -389,6 +389,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void*
     DeviceGuard dg(s->device);
     const bool count = v.bytes != nullptr;
     hipError_t e;
+    if (kernel == VR_KERNEL_AUTO) kernel = VR_KERNEL_TILE;   // measured fastest for every pair
     if (kernel == VR_KERNEL_TILE) {
         e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, (hipStream_t)stream);
     } else {
@@ -512,7 +513,7 @@ int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr
     if (!out_dev) return fail(VR_E_INVALID, "out_dev is NULL");
     if (opts->row_begin > opts->row_end || opts->row_end > height) return fail(VR_E_INVALID, "bad row range");
     if (!opts->nranks || opts->rank >= opts->nranks) return fail(VR_E_INVALID, "bad band partition");
-    if (opts->kernel != VR_KERNEL_PERSISTENT && opts->kernel != VR_KERNEL_TILE) return fail(VR_E_INVALID, "unknown kernel");
+    if (opts->kernel > VR_KERNEL_PERSISTENT) return fail(VR_E_INVALID, "unknown kernel");
     const uint32_t rows = opts->row_end - opts->row_begin;
     const uint32_t band = opts->band_rows ? opts->band_rows : std::max(1u, rows);
     v.row0 = opts->row_begin;
@@ -529,7 +530,7 @@ int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr
 int vr_render(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit, const float translation[3],
               uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin, uint32_t row_end, uint32_t* out_dev,
               void* stream) {
-    vr_render_opts o{VR_KERNEL_PERSISTENT, row_begin, row_end, 0, 0, 1, nullptr};
+    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, nullptr};
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
@@ -544,7 +545,7 @@ int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t band_rows,
                     uint32_t rank, uint32_t nranks, uint32_t* out_dev, void* stream) {
     if (!band_rows) return fail(VR_E_INVALID, "band_rows must be > 0");
-    vr_render_opts o{VR_KERNEL_PERSISTENT, 0, height, band_rows, rank, nranks, nullptr};
+    vr_render_opts o{VR_KERNEL_AUTO, 0, height, band_rows, rank, nranks, nullptr};
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
@@ -552,7 +553,7 @@ int vr_render_count(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin,
                     uint32_t row_end, uint32_t* out_dev, uint64_t* bytes_dev, void* stream) {
     if (!bytes_dev) return fail(VR_E_INVALID, "bytes_dev is NULL");
-    vr_render_opts o{VR_KERNEL_PERSISTENT, row_begin, row_end, 0, 0, 1, bytes_dev};
+    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, bytes_dev};
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 

@@ -50,8 +50,9 @@ struct KView {
 // Launch one render (defined in vr_march.hip).
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,
                         hipStream_t stream);
-// Persistent state-machine kernel (vr_persist.hip); `queue` = 2 zeroed uint32
-// words private to this launch (the kernel leaves them zeroed on exit).
+// Persistent state-machine kernel (vr_persist.hip); `queue` = kQueueWords
+// uint32 private to this launch (zeroed on the stream before the kernel).
+constexpr uint32_t kQueueWords = 8 * 64;
 hipError_t launch_persist(int store, int algo, bool count, const KScene& s, const KView& v, uint32_t* queue,
                           hipStream_t stream);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);

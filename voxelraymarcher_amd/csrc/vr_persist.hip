@@ -325,45 +325,73 @@ struct Machine : Ctx<STORE, COUNT> {
     }
 };
 
+// Work distribution: the frame's 8x8 tiles are split into kShards contiguous
+// stripes; workgroup b starts on stripe b % 8 (workgroups b and b+8 share an
+// XCD under round-robin placement -- speed only, never correctness) and
+// steals from the other stripes when its own is drained.  A wave fetches one
+// whole tile (64 pixels) per atomic into a wave-local pool; lanes whose
+// pixel is done take the next pixel of the pool.  queue[kHeadStride * s] is
+// stripe s's head (zeroed by the host before the launch).
+constexpr uint32_t kShards = 8;
+constexpr uint32_t kHeadStride = 64;     // one head per 256-B line
+
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(256) void persist_kernel(KScene s, KView v, uint32_t* __restrict__ queue) {
     Machine<STORE, ALGO, COUNT> m(s, v);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (v.W + 7u) / 8u;
-    const uint32_t total = tiles_x * ((v.local_rows + 7u) / 8u) * 64u;
-    bool alive = true, has = false;
+    const uint32_t ntiles = tiles_x * ((v.local_rows + 7u) / 8u);
+    const uint32_t home = blockIdx.x % kShards;
+    bool has = false, wave_live = true;
     uint32_t out_idx = 0;
+    uint32_t pool_next = 0, pool_end = 0;      // wave-uniform pixel range
+    uint32_t shard = home;
     for (;;) {
-        for (;;) {   // refill lanes without a pixel (wave-aggregated fetch)
-            const bool need = alive && !has;
+        for (;;) {   // refill lanes without a pixel
+            const bool need = wave_live && !has;
             const uint64_t mask = __ballot(need);
             if (mask == 0) break;
-            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1u;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(queue, (uint32_t)__popcll(mask));
-            base = __shfl(base, (int)leader, 64);
-            if (need) {
-                const uint32_t idx = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-                if (idx >= total) {
-                    alive = false;
-                } else {
-                    const uint32_t t = idx >> 6, w = idx & 63u;
-                    const uint32_t x = (t % tiles_x) * 8u + (w & 7u), l = (t / tiles_x) * 8u + (w >> 3);
-                    if (x < v.W && l < v.local_rows) {
-                        out_idx = l * v.W + x;
-                        const uint32_t band = l / v.band_rows;
-                        const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
-                        if (y >= v.row_limit) {
-                            v.out[out_idx] = 0u;
-                        } else if (m.begin_pixel(x, y)) {
-                            v.out[out_idx] = m.aborted ? 0u : m.result;
-                            m.count(4);
-                        } else {
-                            has = true;
-                        }
+            if (pool_next == pool_end) {
+                uint32_t got = 0xFFFFFFFFu;
+                if (lane == 0) {
+                    for (uint32_t k = 0; k < kShards; ++k) {
+                        const uint32_t sh = (shard + k) % kShards;
+                        const uint32_t t0 = (uint32_t)(((uint64_t)ntiles * sh) / kShards);
+                        const uint32_t t1 = (uint32_t)(((uint64_t)ntiles * (sh + 1)) / kShards);
+                        uint32_t* head = queue + kHeadStride * sh;
+                        if (__hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= t1 - t0) continue;
+                        const uint32_t t = t0 + atomicAdd(head, 1u);
+                        if (t < t1) { got = t; shard = sh; break; }
+                    }
+                }
+                got = __builtin_amdgcn_readfirstlane(got);
+                shard = __builtin_amdgcn_readfirstlane(shard);
+                if (got == 0xFFFFFFFFu) { wave_live = false; break; }
+                pool_next = got * 64u;
+                pool_end = pool_next + 64u;
+            }
+            const uint32_t avail = pool_end - pool_next;
+            const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+            if (need && rank < avail) {
+                const uint32_t idx = pool_next + rank;
+                const uint32_t t = idx >> 6, w = idx & 63u;
+                const uint32_t x = (t % tiles_x) * 8u + (w & 7u), l = (t / tiles_x) * 8u + (w >> 3);
+                if (x < v.W && l < v.local_rows) {
+                    out_idx = l * v.W + x;
+                    const uint32_t band = l / v.band_rows;
+                    const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
+                    if (y >= v.row_limit) {
+                        v.out[out_idx] = 0u;
+                    } else if (m.begin_pixel(x, y)) {
+                        v.out[out_idx] = m.aborted ? 0u : m.result;
+                        m.count(4);
+                    } else {
+                        has = true;
                     }
                 }
             }
+            const uint32_t n = (uint32_t)__popcll(mask);
+            pool_next += n < avail ? n : avail;
         }
         if (!__any(has)) break;
         if (has && m.step()) {
@@ -376,14 +404,6 @@ __global__ __launch_bounds__(256) void persist_kernel(KScene s, KView v, uint32_
         unsigned long long b = m.bytes;
         for (int off = 32; off > 0; off >>= 1) b += __shfl_down(b, off, 64);
         if (lane == 0 && b) atomicAdd(v.bytes, b);
-    }
-    // the last wave out resets the queue slot for the next launch that uses it
-    if (lane == 0) {
-        const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-        if (atomicAdd(queue + 1, 1u) == waves - 1u) {
-            atomicExch(queue, 0u);
-            atomicExch(queue + 1, 0u);
-        }
     }
 }
 
@@ -409,6 +429,8 @@ hipError_t launch_one(const KScene& s, const KView& v, uint32_t* queue, hipStrea
     const uint64_t need = (tiles + 3u) / 4u;      // 4 waves per block, >= 1 tile each
     if (grid > need) grid = need;
     if (grid == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(queue, 0, kShards * kHeadStride * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((persist_kernel<STORE, ALGO, COUNT>), dim3((unsigned)grid), dim3(256), 0, stream, s, v, queue);
     return hipGetLastError();
 }

@@ -207,14 +207,15 @@ def _require_u32(out: torch.Tensor, words: int) -> None:
 
 class Kernel(enum.IntEnum):
     """vr_kernel: which HIP implementation renders (identical pixels)."""
-    PERSISTENT = _capi.VR_KERNEL_PERSISTENT
+    AUTO = _capi.VR_KERNEL_AUTO
     TILE = _capi.VR_KERNEL_TILE
+    PERSISTENT = _capi.VR_KERNEL_PERSISTENT
 
 
 def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
               info: VoxelSceneInfo, width: int, height: int, out: torch.Tensor, row_begin: int = 0,
               row_end: int | None = None, band_rows: int = 0, rank: int = 0, nranks: int = 1,
-              counter: torch.Tensor | None = None, kernel: Kernel = Kernel.PERSISTENT, stream=None) -> torch.Tensor:
+              counter: torch.Tensor | None = None, kernel: Kernel = Kernel.AUTO, stream=None) -> torch.Tensor:
     """vr_render_ex: rows [row_begin,row_end), bands of band_rows (0 = one band) dealt to nranks ranks."""
     row_end = height if row_end is None else row_end
     rows = row_end - row_begin
@@ -233,13 +234,13 @@ def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, 
 def run_raymarching_kernel(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera,
                            lighting: _capi.VrLighting, info: VoxelSceneInfo, width: int, height: int,
                            out: torch.Tensor | None = None, row_begin: int = 0, row_end: int | None = None,
-                           stream=None, kernel: Kernel = Kernel.PERSISTENT) -> torch.Tensor:
+                           stream=None, kernel: Kernel = Kernel.AUTO) -> torch.Tensor:
     """Launch the ray march for rows [row_begin,row_end) (Main.cu:105-163); asynchronous."""
     row_end = height if row_end is None else row_end
     words = (row_end - row_begin) * width
     if out is None:
         out = torch.empty(words, dtype=torch.int32, device=f"cuda:{scene.info()['device']}")
-    if kernel == Kernel.PERSISTENT:
+    if kernel == Kernel.AUTO:
         _require_u32(out, words)
         check(lib().vr_render(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
                               f3(info.translation), int(info.scale), int(width), int(height), int(row_begin),
@@ -252,7 +253,7 @@ def run_raymarching_kernel(scene: DeviceScene, algorithm: RayMarchAlgorithm, cam
 def render_count(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
                  info: VoxelSceneInfo, width: int, height: int, out: torch.Tensor, counter: torch.Tensor,
                  row_begin: int = 0, row_end: int | None = None, stream=None,
-                 kernel: Kernel = Kernel.PERSISTENT) -> None:
+                 kernel: Kernel = Kernel.AUTO) -> None:
     """Instrumented render: adds the SURVEY 8(d) algorithmic bytes into counter (int64 cuda scalar)."""
     render_ex(scene, algorithm, camera, lighting, info, width, height, out, row_begin, row_end,
               counter=counter, kernel=kernel, stream=stream)
