@@ -325,10 +325,18 @@ typedef struct {
     uint64_t bytes;
     uint32_t iters;
     int aborted;
+    int in_shadow;          /* statistics only: counting into st[1] while walking a shadow ray */
+    uint64_t* st;           /* optional work statistics, OR_STAT_* x 2 (primary, shadow) */
 } ctx;
+
+/* work statistics (or_render_stats) */
+enum { OR_STAT_REGION = 0, OR_STAT_EXISTS, OR_STAT_SKIP, OR_STAT_LOOKUP, OR_STAT_PROBE, OR_STAT_HIT,
+       OR_STAT_ITERS, OR_STAT_N };
+#define STAT(c, k) do { if ((c)->st) (c)->st[(c)->in_shadow * OR_STAT_N + (k)]++; } while (0)
 
 static inline int tick(ctx* c) {
     if (c->aborted) return 0;
+    STAT(c, OR_STAT_ITERS);
     if (++c->iters > VR_ITER_BUDGET) { c->aborted = 1; return 0; }
     return 1;
 }
@@ -343,6 +351,7 @@ static inline int32_t region_at(ctx* c, v3i r) {
     uint32_t D = c->s->D, mc = (uint32_t)c->s->min_coord;
     uint32_t ux = (uint32_t)r.v[0] - mc, uy = (uint32_t)r.v[1] - mc, uz = (uint32_t)r.v[2] - mc;
     c->bytes += 4;
+    STAT(c, OR_STAT_REGION);
     return c->s->region_slot[ux + uy * D + uz * D * D];
 }
 
@@ -353,9 +362,12 @@ static inline int32_t region_at(ctx* c, v3i r) {
 static inline int space_exists(ctx* c, int32_t reg, int32_t x, int32_t y, int32_t z) {
     if (c->s->store != OR_STORE_VCS) return 1;
     c->bytes += 4;
+    STAT(c, OR_STAT_EXISTS);
     int32_t cid = cluster_id_short(x, y, z);
-    if (cid < 0 || cid >= 512) return 0;
-    return c->s->vcs_dir[(size_t)reg * 512 + (size_t)cid] >= 0;
+    if (cid < 0 || cid >= 512) { STAT(c, OR_STAT_SKIP); return 0; }
+    if (c->s->vcs_dir[(size_t)reg * 512 + (size_t)cid] >= 0) return 1;
+    STAT(c, OR_STAT_SKIP);
+    return 0;
 }
 
 /* VoxelClusterStore::lookupVoxel + performBinarySearch (VoxelClusterStore.cuh:101-135)
@@ -363,6 +375,7 @@ static inline int space_exists(ctx* c, int32_t reg, int32_t x, int32_t y, int32_
 static uint32_t lookup_voxel(ctx* c, int32_t reg, int32_t x, int32_t y, int32_t z) {
     const or_scene* s = c->s;
     uint32_t key = or_generate_3d_point((uint32_t)x, (uint32_t)y, (uint32_t)z);
+    STAT(c, OR_STAT_LOOKUP);
     if (s->store == OR_STORE_VCS) {
         int32_t cid = cluster_id_short(x, y, z);
         if (cid < 0 || cid >= 512) return EMPTY_VAL;
@@ -376,7 +389,8 @@ static uint32_t lookup_voxel(ctx* c, int32_t reg, int32_t x, int32_t y, int32_t 
             int32_t mid = low + (high - low) / 2;
             uint32_t k = blk[mid * 2 + 1];
             c->bytes += 4;
-            if (k == key) { c->bytes += 4; return blk[mid * 2 + 2]; }
+            STAT(c, OR_STAT_PROBE);
+            if (k == key) { c->bytes += 4; STAT(c, OR_STAT_HIT); return blk[mid * 2 + 2]; }
             if (k < key) low = mid + 1; else high = mid - 1;
         }
         return EMPTY_VAL;
@@ -385,10 +399,12 @@ static uint32_t lookup_voxel(ctx* c, int32_t reg, int32_t x, int32_t y, int32_t 
         uint32_t M = t->M;
         uint32_t k1 = ((uint32_t)or_hash1((int32_t)key, t->offset) % M + M) % M;
         c->bytes += 4;
-        if (t->k1[k1] == key) { c->bytes += 4; return t->v1[k1]; }
+        STAT(c, OR_STAT_PROBE);
+        if (t->k1[k1] == key) { c->bytes += 4; STAT(c, OR_STAT_HIT); return t->v1[k1]; }
         uint32_t k2 = ((uint32_t)or_hash2((int32_t)key, t->prime) % M + M) % M;
         c->bytes += 4;
-        if (t->k2[k2] == key) { c->bytes += 4; return t->v2[k2]; }
+        STAT(c, OR_STAT_PROBE);
+        if (t->k2[k2] == key) { c->bytes += 4; STAT(c, OR_STAT_HIT); return t->v2[k2]; }
         return EMPTY_VAL;
     }
 }
@@ -540,6 +556,7 @@ static uint32_t shadow_grid_original(ctx* c, ray3* ray, int32_t reg) {
 /* isInShadowOriginalRayMarch (Renderer.cuh:174-235) */
 static int shadow_scene_original(ctx* c, ray3 lr, v3i cr) {
     if (!c->lit->use_shadows) return 0;
+    c->in_shadow = 1;
     while (in_scene(c, cr)) {
         if (!tick(c)) return 0;
         int32_t reg = region_at(c, cr);
@@ -754,6 +771,7 @@ static uint32_t grid_longest(ctx* c, ray3* orig, v3f rwp, int32_t reg, v3i cr, i
 /* isInShadowRayMarchVoxelSceneLongestAxis (Renderer.cuh:633-694) */
 static int shadow_scene_longest(ctx* c, ray3 lr, v3i cr) {
     if (!c->lit->use_shadows) return 0;
+    c->in_shadow = 1;
     while (in_scene(c, cr)) {
         if (!tick(c)) return 0;
         int32_t reg = region_at(c, cr);
@@ -849,7 +867,7 @@ void or_lighting_default(or_lighting* out) {
  * then the kernel body (Renderer.cuh:1033-1063). */
 static uint32_t render_pixel(const or_scene* s, int algo, const or_camera* cam, const or_lighting* lit,
                              v3f tr, uint32_t scale, uint32_t W, uint32_t H, uint32_t x, uint32_t y,
-                             uint64_t* bytes) {
+                             uint64_t* bytes, uint64_t* st) {
     float u = ((float)x + 0.5f) / (float)W;
     float v = ((float)(H - y) + 0.5f) / (float)H;
     v3f llc = V3(cam->lower_left[0], cam->lower_left[1], cam->lower_left[2]);
@@ -859,7 +877,7 @@ static uint32_t render_pixel(const or_scene* s, int algo, const or_camera* cam, 
     v3f ro = vadd(vadd(llc, vscale(u, hor)), vscale(v, ver));
     ray3 world = {ro, vunit(vsub(ro, org))};
     ctx c; memset(&c, 0, sizeof c);
-    c.s = s; c.lit = lit; c.translation = tr;
+    c.s = s; c.lit = lit; c.translation = tr; c.st = st;
     uint32_t col = scene_march(&c, world, scale, algo);
     if (c.aborted) col = 0;
     c.bytes += 4;                /* the pixel write */
@@ -883,7 +901,7 @@ int or_render(const or_scene* s, int algo, const or_camera* cam, const or_lighti
         uint32_t y = row_begin + (uint32_t)r;
         for (uint32_t x = 0; x < width; ++x) {
             uint64_t b = 0;
-            out[(size_t)r * width + x] = render_pixel(s, algo, cam, lit, tr, scale, width, height, x, y, &b);
+            out[(size_t)r * width + x] = render_pixel(s, algo, cam, lit, tr, scale, width, height, x, y, &b, NULL);
             total += b;
         }
     }
@@ -901,8 +919,26 @@ int or_render_pixels(const or_scene* s, int algo, const or_camera* cam, const or
                 translation ? translation[2] : 0.0f);
     for (size_t i = 0; i < n; ++i) {
         uint64_t b = 0;
-        out[i] = render_pixel(s, algo, cam, lit, tr, scale, width, height, px[i], py[i], &b);
+        out[i] = render_pixel(s, algo, cam, lit, tr, scale, width, height, px[i], py[i], &b, NULL);
         if (bytes_per_pixel) bytes_per_pixel[i] = b;
     }
+    return 0;
+}
+
+/* Work statistics of rows [row_begin,row_end): st[2*OR_STAT_N] = counts of
+ * region reads, existence checks, cluster skips, lookups, probes, hits and
+ * loop iterations, for primary (st[0..6]) and shadow (st[7..13]) walks. */
+int or_render_stats(const or_scene* s, int algo, const or_camera* cam, const or_lighting* lit,
+                    const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
+                    uint32_t row_begin, uint32_t row_end, uint64_t* st) {
+    if (!s || !cam || !lit || !st) return -1;
+    v3f tr = V3(translation ? translation[0] : 0.0f, translation ? translation[1] : 0.0f,
+                translation ? translation[2] : 0.0f);
+    memset(st, 0, sizeof(uint64_t) * 2 * OR_STAT_N);
+    for (uint32_t y = row_begin; y < row_end; ++y)
+        for (uint32_t x = 0; x < width; ++x) {
+            uint64_t b = 0;
+            (void)render_pixel(s, algo, cam, lit, tr, scale, width, height, x, y, &b, st);
+        }
     return 0;
 }

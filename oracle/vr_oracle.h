@@ -95,6 +95,12 @@ int or_render_pixels(const or_scene* s, int algo, const or_camera* cam, const or
                      const uint32_t* px, const uint32_t* py, size_t n, uint32_t* out,
                      uint64_t* bytes_per_pixel);
 
+/* Work statistics (single-threaded): 2 x 7 counters, primary then shadow:
+ * region reads, existence checks, cluster skips, lookups, key probes, hits, loop iterations. */
+int or_render_stats(const or_scene* s, int algo, const or_camera* cam, const or_lighting* lit,
+                    const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
+                    uint32_t row_begin, uint32_t row_end, uint64_t* st);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,6 +82,9 @@ __device__ __forceinline__ uint32_t hash2(uint32_t k, uint32_t prime) {
     return k;
 }
 
+typedef uint2 Blk;    // VCS directory entry {block offset (16-B units), n}
+__device__ __forceinline__ bool absent(Blk b) { return b.x == kNone; }
+
 struct Hit {
     uint32_t lit;       // lit colour before the shadow multiply
     f3 so;              // shadow-ray origin (region-local)
@@ -122,34 +125,104 @@ struct Ctx {
 
     // doesVoxelSpaceExist (StorageStructure.cuh:29-32,49-52) ->
     // VoxelClusterStore::doesClusterExist (VoxelClusterStore.cuh:93-99).
-    // Returns the cluster block offset (VCS) or 0 (hashtable), kNone = absent.
-    __device__ __forceinline__ uint32_t exists(uint32_t reg, int32_t x, int32_t y, int32_t z) {
-        if (STORE == STORE_HASH) return 0u;
+    // Returns the directory entry {block offset, n} (VCS) or {0,0} (hashtable:
+    // the space always exists); absent() = no cluster.
+    __device__ __forceinline__ Blk exists(uint32_t reg, int32_t x, int32_t y, int32_t z) {
+        if (STORE == STORE_HASH) return Blk{0u, 0u};
         count(4);
         uint32_t c = (((uint32_t)x >> 3) << 6) | (((uint32_t)y >> 3) << 3) | ((uint32_t)z >> 3);
         int32_t cid = (int32_t)(int16_t)(uint16_t)c;      // `short` getVoxelClusterID
-        if (cid < 0 || cid >= 512) return kNone;          // past the reference's directory
+        if (cid < 0 || cid >= 512) return Blk{kNone, 0u}; // past the reference's directory
         return s.vcs_dir[reg * 512u + (uint32_t)cid];
     }
 
-    // VoxelClusterStore::lookupVoxel / performBinarySearch (VoxelClusterStore.cuh:101-135),
-    // CuckooHashTable::lookupVoxel (CuckooHashTable.cuh:59-76).
-    __device__ __forceinline__ uint32_t lookup(uint32_t reg, uint32_t blk, int32_t x, int32_t y, int32_t z) {
-        uint32_t key = ((uint32_t)x << 20) | ((uint32_t)y << 10) | (uint32_t)z;   // generate3DPoint
-        if (STORE == STORE_VCS) {
-            const uint32_t* b = s.vcs_pool + blk;
-            uint32_t n = b[0];
+    // Reference binary-search probes for a key of rank `rank` (number of keys
+    // < q) among n sorted keys: key[mid] < q <=> mid < rank, key[mid] == q <=>
+    // found && mid == rank (performBinarySearch, VoxelClusterStore.cuh:101-126).
+    // Only the COUNT instantiations evaluate it (SURVEY 8(d) bytes).
+    __device__ __forceinline__ void count_bsearch(uint32_t n, uint32_t rank, bool found) {
+        if (!COUNT) return;
+        int32_t low = 0, high = (int32_t)n - 1;
+        uint32_t probes = 0;
+        while (low <= high) {
+            int32_t mid = low + ((high - low) >> 1);
+            ++probes;
+            if (found && (uint32_t)mid == rank) break;
+            if ((uint32_t)mid < rank) low = mid + 1; else high = mid - 1;
+        }
+        count(4 + 4 * probes + (found ? 4 : 0));
+    }
+
+    // A coordinate outside [0,64) whose `short` cluster id still lands in the
+    // directory (longest-axis walks can probe one): the reference binary-searches
+    // the full key x<<20|y<<10|z, which no key of the block can equal.  Rare;
+    // run the reference search verbatim over the block's keys widened back to
+    // full keys, so the probe count (COUNT) is exact too.
+    __device__ uint32_t lookup_aliased(const uint4* b, VcsGeom gm, uint32_t n, int32_t x,
+                                                                 int32_t y, int32_t z) {
+        const uint32_t ux = (uint32_t)x, uy = (uint32_t)y, uz = (uint32_t)z;
+        const uint32_t K = (ux << 20) | (uy << 10) | uz;
+        const uint32_t c = (((ux >> 3) << 6) | ((uy >> 3) << 3) | (uz >> 3)) & 0x1FFu;
+        const uint32_t bx = (c >> 6) * 8u, by = ((c >> 3) & 7u) * 8u, bz = (c & 7u) * 8u;
+        const uint16_t* k16 = reinterpret_cast<const uint16_t*>(b + gm.u_keys);
+        count(4);
+        int32_t low = 0, high = (int32_t)n - 1;
+        while (low <= high) {
+            int32_t mid = low + ((high - low) >> 1);
+            const uint32_t c9 = k16[mid];
+            const uint32_t full = ((bx + (c9 >> 6)) << 20) | ((by + ((c9 >> 3) & 7u)) << 10) | (bz + (c9 & 7u));
             count(4);
-            int32_t low = 0, high = (int32_t)n - 1;
-            while (low <= high) {
-                int32_t mid = low + ((high - low) >> 1);
-                uint32_t k = b[1 + mid];
-                count(4);
-                if (k == key) { count(4); return b[1 + n + (uint32_t)mid]; }
-                if (k < key) low = mid + 1; else high = mid - 1;
+            if (full == K) { count(4); return reinterpret_cast<const uint32_t*>(b + gm.u_vals)[mid]; }
+            if (full < K) low = mid + 1; else high = mid - 1;
+        }
+        return kEmpty;
+    }
+
+    // Number of the 8 16-bit keys of a node that are < q.
+    __device__ __forceinline__ static uint32_t count_lt(uint4 nd, uint32_t q) {
+        uint32_t c = 0;
+        c += (nd.x & 0xFFFFu) < q; c += (nd.x >> 16) < q;
+        c += (nd.y & 0xFFFFu) < q; c += (nd.y >> 16) < q;
+        c += (nd.z & 0xFFFFu) < q; c += (nd.z >> 16) < q;
+        c += (nd.w & 0xFFFFu) < q; c += (nd.w >> 16) < q;
+        return c;
+    }
+    __device__ __forceinline__ static uint32_t key_at(uint4 nd, uint32_t j) {
+        uint32_t w = j < 4u ? (j < 2u ? nd.x : nd.y) : (j < 6u ? nd.z : nd.w);
+        return (j & 1u) ? (w >> 16) : (w & 0xFFFFu);
+    }
+
+    // VoxelClusterStore::lookupVoxel / performBinarySearch (VoxelClusterStore.cuh:101-135):
+    // the same search over the cluster's sorted keys, widened to one 16-B node
+    // of 8 keys per level (9-ary): 1 node load for n <= 8, 2 for n <= 64, 3 for
+    // n <= 512 instead of 1 + ~log2(n) dependent word loads.  Identical result.
+    // CuckooHashTable::lookupVoxel (CuckooHashTable.cuh:59-76).
+    __device__ __forceinline__ uint32_t lookup(uint32_t reg, Blk blk, int32_t x, int32_t y, int32_t z) {
+        if (STORE == STORE_VCS) {
+            const uint32_t n = blk.y;
+            const VcsGeom gm = vcs_geom(n);
+            const uint4* b = s.vcs_pool + blk.x;
+            if (((uint32_t)x | (uint32_t)y | (uint32_t)z) >= 64u) return lookup_aliased(b, gm, n, x, y, z);
+            const uint32_t q = (((uint32_t)x & 7u) << 6) | (((uint32_t)y & 7u) << 3) | ((uint32_t)z & 7u);
+            uint32_t grp = 0, chunk = 0;
+            if (gm.groups > 1u) {
+                grp = count_lt(b[0], q);
+                if (grp >= gm.groups) { count_bsearch(n, n, false); return kEmpty; }
             }
-            return kEmpty;
+            if (gm.chunks > 1u) {
+                const uint32_t cl = count_lt(b[gm.u_f1 + grp], q);
+                const uint32_t in_grp = min(8u, gm.chunks - 8u * grp);
+                if (cl >= in_grp) { count_bsearch(n, n, false); return kEmpty; }
+                chunk = 8u * grp + cl;
+            }
+            const uint4 leaf = b[gm.u_keys + chunk];
+            const uint32_t r = count_lt(leaf, q);
+            const bool found = r < 8u && key_at(leaf, r) == q;
+            count_bsearch(n, min(8u * chunk + r, n), found);
+            if (!found) return kEmpty;
+            return reinterpret_cast<const uint32_t*>(b + gm.u_vals)[8u * chunk + r];
         } else {
+            const uint32_t key = ((uint32_t)x << 20) | ((uint32_t)y << 10) | (uint32_t)z;   // generate3DPoint
             uint4 m = s.ht_meta[reg];          // {base, M, prime, offset}
             uint32_t s1 = hash1(key, m.w) % m.y;
             count(4);

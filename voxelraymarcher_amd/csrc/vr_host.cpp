@@ -248,14 +248,19 @@ int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* 
     if (rc_up) { free_scene(s); return rc_up; }
 
     if (store == VR_STORE_VCS) {
-        // VoxelClusterStore ctor (VoxelClusterStore.cuh:37-85), SoA blocks.
-        std::vector<uint32_t> dir((size_t)nr * 512, vr::kNone);
-        std::vector<uint32_t> pool;
-        pool.reserve(2 * m + 16);
+        // VoxelClusterStore ctor (VoxelClusterStore.cuh:37-85): per region a
+        // 512-entry directory and, per non-empty cluster, its keys in ascending
+        // order -- stored as 16-bit in-cluster indices (same order as the full
+        // keys inside one cluster) in a static 9-ary tree of 16-B nodes, then
+        // the values (vr_internal.h "VCS").
+        std::vector<uint2> dir((size_t)nr * 512, uint2{vr::kNone, 0u});
+        std::vector<uint32_t> pool;   // 4 words per 16-B unit
+        pool.reserve(2 * m + 4096);
         std::vector<uint32_t> cid_of;
+        std::vector<uint32_t> order;
         for (uint32_t r = 0; r < nr; ++r) {
             size_t b = region_begin[r], e = region_begin[r + 1];
-            uint32_t counts[512] = {0};
+            uint32_t counts[512] = {0}, first[513];
             cid_of.resize(e - b);
             for (size_t i = b; i < e; ++i) {
                 uint32_t key = (uint32_t)recs[i].k;
@@ -264,25 +269,47 @@ int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* 
                 cid_of[i - b] = c;
                 counts[c]++;
             }
-            uint32_t pos[512];
-            for (uint32_t c = 0; c < 512; ++c) {
-                if (!counts[c]) continue;
-                if (pool.size() + 1 + 2 * (size_t)counts[c] >= 0xFFFFFFFFull) { free_scene(s); return fail(VR_E_BUILD, "VCS pool exceeds 32-bit offsets"); }
-                dir[(size_t)r * 512 + c] = (uint32_t)pool.size();
-                pool.push_back(counts[c]);
-                pos[c] = (uint32_t)pool.size();
-                pool.resize(pool.size() + 2 * (size_t)counts[c]);
-            }
+            first[0] = 0;
+            for (uint32_t c = 0; c < 512; ++c) first[c + 1] = first[c] + counts[c];
+            order.assign(e - b, 0);
             uint32_t fill[512] = {0};
-            for (size_t i = b; i < e; ++i) {        // keys arrive ascending: blocks stay sorted
+            for (size_t i = b; i < e; ++i) {      // keys arrive ascending: stable bucket keeps them sorted
                 uint32_t c = cid_of[i - b];
-                pool[pos[c] + fill[c]] = (uint32_t)recs[i].k;
-                pool[pos[c] + counts[c] + fill[c]] = recs[i].val;
-                fill[c]++;
+                order[first[c] + fill[c]++] = (uint32_t)(i - b);
+            }
+            for (uint32_t c = 0; c < 512; ++c) {
+                const uint32_t n = counts[c];
+                if (!n) continue;
+                const vr::VcsGeom gm = vr::vcs_geom(n);
+                if (pool.size() / 4 + gm.units >= 0xFFFFFFFFull) { free_scene(s); return fail(VR_E_BUILD, "VCS pool exceeds 32-bit offsets"); }
+                const size_t base = pool.size();
+                dir[(size_t)r * 512 + c] = uint2{(uint32_t)(base / 4), n};
+                pool.resize(base + 4 * (size_t)gm.units, 0u);
+                uint16_t* k16 = reinterpret_cast<uint16_t*>(pool.data() + base);
+                uint32_t* vals = pool.data() + base + 4 * (size_t)gm.u_vals;
+                std::vector<uint16_t> keys(8 * (size_t)gm.chunks, 0xFFFFu);
+                for (uint32_t j = 0; j < n; ++j) {
+                    const Rec& rc = recs[b + order[first[c] + j]];
+                    uint32_t key = (uint32_t)rc.k;
+                    uint32_t x = key >> 20, y = (key >> 10) & 0x3FFu, z = key & 0x3FFu;
+                    keys[j] = (uint16_t)(((x & 7u) << 6) | ((y & 7u) << 3) | (z & 7u));
+                    vals[j] = rc.val;
+                }
+                auto chunk_max = [&](uint32_t ch) { return keys[std::min<size_t>(8 * (size_t)ch + 7, n - 1)]; };
+                if (gm.groups > 1)                 // F0: max key of each 64-key group
+                    for (uint32_t g = 0; g < 8; ++g)
+                        k16[g] = g < gm.groups ? keys[std::min<size_t>(64 * (size_t)g + 63, n - 1)] : 0xFFFFu;
+                if (gm.chunks > 1)                 // F1: max key of each chunk, one node per group
+                    for (uint32_t g = 0; g < gm.groups; ++g)
+                        for (uint32_t j = 0; j < 8; ++j) {
+                            uint32_t ch = 8 * g + j;
+                            k16[8 * (gm.u_f1 + g) + j] = ch < gm.chunks ? chunk_max(ch) : 0xFFFFu;
+                        }
+                for (size_t j = 0; j < keys.size(); ++j) k16[8 * (size_t)gm.u_keys + j] = keys[j];
             }
         }
-        if (pool.empty()) pool.push_back(0);
-        if ((rc_up = upload(s->vcs_dir, dir.data(), dir.size() * 4)) ||
+        if (pool.empty()) pool.assign(4, 0u);
+        if ((rc_up = upload(s->vcs_dir, dir.data(), dir.size() * sizeof(uint2))) ||
             (rc_up = upload(s->vcs_pool, pool.data(), pool.size() * 4))) {
             free_scene(s);
             return rc_up;
@@ -323,8 +350,8 @@ int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* 
 vr::KScene kscene(const vr_scene* s) {
     vr::KScene k{};
     k.region_slot = (const uint32_t*)s->region_slot.p;
-    k.vcs_dir = (const uint32_t*)s->vcs_dir.p;
-    k.vcs_pool = (const uint32_t*)s->vcs_pool.p;
+    k.vcs_dir = (const uint2*)s->vcs_dir.p;
+    k.vcs_pool = (const uint4*)s->vcs_pool.p;
     k.ht_meta = (const uint4*)s->ht_meta.p;
     k.ht_slots = (const uint2*)s->ht_slots.p;
     k.D = s->D;

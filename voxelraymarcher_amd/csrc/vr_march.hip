@@ -50,8 +50,8 @@ struct Walker : Ctx<STORE, COUNT> {
         while (in_region(o)) {
             if (!tick()) return false;
             int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-            uint32_t blk = exists(reg, vx, vy, vz);
-            if (blk == kNone) {
+            Blk blk = exists(reg, vx, vy, vz);
+            if (absent(blk)) {
                 // cluster skip; block-scoped t values (stale outer ones)
                 int32_t cx = px ? ((vx / 8) + 1) * 8 : (vx / 8) * 8;
                 int32_t cy = py ? ((vy / 8) + 1) * 8 : (vy / 8) * 8;
@@ -110,8 +110,8 @@ struct Walker : Ctx<STORE, COUNT> {
     template <bool SHADOW>
     __device__ int jump(f3& oo, LA& a, uint32_t reg, f3 rwp, i3 cr, Hit& h) {
         float tX = 0.0f, tY = 0.0f, tZ = 0.0f, tMin = 0.0f;
-        uint32_t blk;
-        while ((blk = exists(reg, a.g.x, a.g.y, a.g.z)) == kNone) {
+        Blk blk;
+        while (absent(blk = exists(reg, a.g.x, a.g.y, a.g.z))) {
             if (!tick()) return 0;
             int32_t nx = a.ds.x > 0.0f ? ((a.g.x / 8) + 1) * 8 : (a.g.x / 8) * 8;
             int32_t ny = a.ds.y > 0.0f ? ((a.g.y / 8) + 1) * 8 : (a.g.y / 8) * 8;
@@ -151,8 +151,8 @@ struct Walker : Ctx<STORE, COUNT> {
     __device__ int axis_step(f3& oo, LA& a, uint32_t axis, bool long_axis, uint32_t reg, f3 rwp, i3 cr,
                              Hit& h, bool& res) {
         seti(a.g, axis, geti(a.g, axis) + geti(a.ad, axis));
-        uint32_t blk = exists(reg, a.g.x, a.g.y, a.g.z);
-        if (blk == kNone) {
+        Blk blk = exists(reg, a.g.x, a.g.y, a.g.z);
+        if (absent(blk)) {
             int jr = jump<SHADOW>(oo, a, reg, rwp, cr, h);
             if (aborted) { res = false; return 1; }
             if (jr != 2) { res = jr == 1; return 1; }

@@ -181,8 +181,8 @@ struct Machine : Ctx<STORE, COUNT> {
         if (!tick()) return finish(0);
         const bool gd = shadow;
         int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-        uint32_t blk = exists(reg, vx, vy, vz);
-        if (blk == kNone) {               // cluster skip (:290-306), block-scoped t values
+        Blk blk = exists(reg, vx, vy, vz);
+        if (absent(blk)) {               // cluster skip (:290-306), block-scoped t values
             int32_t cx = d.x > 0.0f ? ((vx / 8) + 1) * 8 : (vx / 8) * 8;
             int32_t cy = d.y > 0.0f ? ((vy / 8) + 1) * 8 : (vy / 8) * 8;
             int32_t cz = d.z > 0.0f ? ((vz / 8) + 1) * 8 : (vz / 8) * 8;
@@ -250,8 +250,8 @@ struct Machine : Ctx<STORE, COUNT> {
         queue >>= 2;
         --qlen;
         seti(g, axis, geti(g, axis) + geti(ad, axis));
-        uint32_t blk = exists(reg, g.x, g.y, g.z);
-        if (blk == kNone) {               // -> performVoxelSpaceJump
+        Blk blk = exists(reg, g.x, g.y, g.z);
+        if (absent(blk)) {               // -> performVoxelSpaceJump
             tX = tY = tZ = tMin = 0.0f;
             qlen = 0;
             phase = P_JUMP;
@@ -279,8 +279,8 @@ struct Machine : Ctx<STORE, COUNT> {
 
     // P_JUMP: one iteration of performVoxelSpaceJump's `while (!doesVoxelSpaceExist)`.
     __device__ int jump_step() {
-        uint32_t blk = exists(reg, g.x, g.y, g.z);
-        if (blk == kNone) {
+        Blk blk = exists(reg, g.x, g.y, g.z);
+        if (absent(blk)) {
             if (!tick()) return finish(0);
             int32_t nx = ds.x > 0.0f ? ((g.x / 8) + 1) * 8 : (g.x / 8) * 8;
             int32_t ny = ds.y > 0.0f ? ((g.y / 8) + 1) * 8 : (g.y / 8) * 8;
