@@ -86,8 +86,9 @@ typedef uint2 Blk;    // VCS directory entry {block offset (16-B units), n}
 __device__ __forceinline__ bool absent(Blk b) { return b.x == kNone; }
 
 struct Hit {
-    uint32_t lit;       // lit colour before the shadow multiply
-    f3 so;              // shadow-ray origin (region-local)
+    uint32_t col;       // the voxel's stored colour
+    f3 n;               // surface normal for the lighting
+    f3 so;              // hit location (region-local): lighting point and shadow-ray origin
     i3 region;          // currentRegion at the hit
     bool longest;       // isInShadowRayMarchVoxelSceneLongestAxis vs ...Original
 };

@@ -29,73 +29,57 @@ struct Walker : Ctx<STORE, COUNT> {
     __device__ Walker(const KScene& s_, const KView& v_) : C(s_, v_) {}
 
     // rayMarchVoxelGrid (Renderer.cuh:260-336) and, SHADOW, shadowRayMarchVoxelGrid (:100-172).
+    // The cluster-skip step (:290-306) and the voxel step (:318-331) share one
+    // code path: both are o += (min_i (target_i - o_i) / d_i + EPSILON) * d with
+    // target = the cluster plane (int, no EPSILON) or ceilf/floorf(o) +- EPSILON;
+    // only the voxel step refreshes the t values the hit normal reads (the skip
+    // branch's are block-scoped).  One set of IEEE divisions per
+    // iteration instead of two divergent ones.  Lighting is applied by the
+    // caller after the walk (Hit carries colour, normal and position).
     template <bool SHADOW>
-    __device__ bool grid_original(f3& o, f3 d, uint32_t reg, f3 rwp, i3 cr, Hit& h) {
+    __device__ bool grid_original(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h) {
         const bool px = d.x > 0.0f, py = d.y > 0.0f, pz = d.z > 0.0f;
+        const bool zx = SHADOW && d.x == 0.0f, zy = SHADOW && d.y == 0.0f, zz = SHADOW && d.z == 0.0f;
         float nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
         float nY = py ? ceilf(o.y) + kEps : floorf(o.y) - kEps;
         float nZ = pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps;
-        float tX, tY, tZ;
-        if (SHADOW) {
-            tX = d.x != 0.0f ? (nX - o.x) / d.x : kInf;
-            tY = d.y != 0.0f ? (nY - o.y) / d.y : kInf;
-            tZ = d.z != 0.0f ? (nZ - o.z) / d.z : kInf;
-        } else {
-            tX = (nX - o.x) / d.x;
-            tY = (nY - o.y) / d.y;
-            tZ = (nZ - o.z) / d.z;
-        }
+        float tX = zx ? kInf : (nX - o.x) / d.x;
+        float tY = zy ? kInf : (nY - o.y) / d.y;
+        float tZ = zz ? kInf : (nZ - o.z) / d.z;
         float tMin = fminf(tX, fminf(tY, tZ));
         o = add(o, scl(tMin + kEps, d));
+        uint32_t col = kEmpty;
         while (in_region(o)) {
             if (!tick()) return false;
-            int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-            Blk blk = exists(reg, vx, vy, vz);
-            if (absent(blk)) {
-                // cluster skip; block-scoped t values (stale outer ones)
-                int32_t cx = px ? ((vx / 8) + 1) * 8 : (vx / 8) * 8;
-                int32_t cy = py ? ((vy / 8) + 1) * 8 : (vy / 8) * 8;
-                int32_t cz = pz ? ((vz / 8) + 1) * 8 : (vz / 8) * 8;
-                float sX, sY, sZ;
-                if (SHADOW) {
-                    sX = d.x != 0.0f ? ((float)cx - o.x) / d.x : kInf;
-                    sY = d.y != 0.0f ? ((float)cy - o.y) / d.y : kInf;
-                    sZ = d.z != 0.0f ? ((float)cz - o.z) / d.z : kInf;
-                } else {
-                    sX = ((float)cx - o.x) / d.x;
-                    sY = ((float)cy - o.y) / d.y;
-                    sZ = ((float)cz - o.z) / d.z;
-                }
-                float sMin = fminf(sX, fminf(sY, sZ));
-                o = add(o, scl(sMin + kEps, d));
-                continue;
+            const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
+            const Blk blk = exists(reg, vx, vy, vz);
+            const bool skip = absent(blk);
+            if (!skip) {
+                col = lookup(reg, blk, vx, vy, vz);
+                if (col != kEmpty) break;
             }
-            uint32_t col = lookup(reg, blk, vx, vy, vz);
-            if (col != kEmpty) {
-                if (!SHADOW) {
-                    h.lit = lighting(col, normal_from_t(tX, tY, tZ, tMin, d), rwp, o);
-                    h.so = o;
-                    h.region = cr;
-                    h.longest = false;
-                }
-                return true;
-            }
-            nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
-            nY = py ? ceilf(o.y) + kEps : floorf(o.y) - kEps;
-            nZ = pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps;
-            if (SHADOW) {
-                tX = d.x != 0.0f ? (nX - o.x) / d.x : kInf;
-                tY = d.y != 0.0f ? (nY - o.y) / d.y : kInf;
-                tZ = d.z != 0.0f ? (nZ - o.z) / d.z : kInf;
-            } else {
-                tX = (nX - o.x) / d.x;
-                tY = (nY - o.y) / d.y;
-                tZ = (nZ - o.z) / d.z;
-            }
-            tMin = fminf(tX, fminf(tY, tZ));
-            o = add(o, scl(tMin + kEps, d));
+            const float cX = (float)(px ? ((vx / 8) + 1) * 8 : (vx / 8) * 8);
+            const float cY = (float)(py ? ((vy / 8) + 1) * 8 : (vy / 8) * 8);
+            const float cZ = (float)(pz ? ((vz / 8) + 1) * 8 : (vz / 8) * 8);
+            nX = skip ? cX : (px ? ceilf(o.x) + kEps : floorf(o.x) - kEps);
+            nY = skip ? cY : (py ? ceilf(o.y) + kEps : floorf(o.y) - kEps);
+            nZ = skip ? cZ : (pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps);
+            const float sX = zx ? kInf : (nX - o.x) / d.x;
+            const float sY = zy ? kInf : (nY - o.y) / d.y;
+            const float sZ = zz ? kInf : (nZ - o.z) / d.z;
+            const float sMin = fminf(sX, fminf(sY, sZ));
+            if (!skip) { tX = sX; tY = sY; tZ = sZ; tMin = sMin; }
+            o = add(o, scl(sMin + kEps, d));
         }
-        return false;
+        if (col == kEmpty) return false;
+        if (!SHADOW) {
+            h.col = col;
+            h.n = normal_from_t(tX, tY, tZ, tMin, d);
+            h.so = o;
+            h.region = cr;
+            h.longest = false;
+        }
+        return true;
     }
 
     // State of one longest-axis region walk (Renderer.cuh:760-915 / :495-631).
@@ -108,7 +92,7 @@ struct Walker : Ctx<STORE, COUNT> {
     // performVoxelSpaceJump (Renderer.cuh:696-751) / performShadowVoxelSpaceJump (:441-492).
     // Returns 0 = EMPTY_VAL (left region / aborted), 1 = hit, 2 = CONTINUE_VAL.
     template <bool SHADOW>
-    __device__ int jump(f3& oo, LA& a, uint32_t reg, f3 rwp, i3 cr, Hit& h) {
+    __device__ int jump(f3& oo, LA& a, uint32_t reg, i3 cr, Hit& h) {
         float tX = 0.0f, tY = 0.0f, tZ = 0.0f, tMin = 0.0f;
         Blk blk;
         while (absent(blk = exists(reg, a.g.x, a.g.y, a.g.z))) {
@@ -130,7 +114,8 @@ struct Walker : Ctx<STORE, COUNT> {
         uint32_t col = lookup(reg, blk, a.g.x, a.g.y, a.g.z);
         if (col != kEmpty) {
             if (!SHADOW) {
-                h.lit = lighting(col, normal_from_t(tX, tY, tZ, tMin, a.ds), rwp, a.old_o);
+                h.col = col;
+                h.n = normal_from_t(tX, tY, tZ, tMin, a.ds);
                 h.so = a.old_o;
                 h.region = cr;
                 h.longest = true;
@@ -148,12 +133,12 @@ struct Walker : Ctx<STORE, COUNT> {
     // One "grid += diff; exists? else jump; lookup; hit" block
     // (Renderer.cuh:807-901 / :542-617).  0 = go on, 1 = return *res, 2 = continue.
     template <bool SHADOW>
-    __device__ int axis_step(f3& oo, LA& a, uint32_t axis, bool long_axis, uint32_t reg, f3 rwp, i3 cr,
+    __device__ int axis_step(f3& oo, LA& a, uint32_t axis, bool long_axis, uint32_t reg, i3 cr,
                              Hit& h, bool& res) {
         seti(a.g, axis, geti(a.g, axis) + geti(a.ad, axis));
         Blk blk = exists(reg, a.g.x, a.g.y, a.g.z);
         if (absent(blk)) {
-            int jr = jump<SHADOW>(oo, a, reg, rwp, cr, h);
+            int jr = jump<SHADOW>(oo, a, reg, cr, h);
             if (aborted) { res = false; return 1; }
             if (jr != 2) { res = jr == 1; return 1; }
             return 2;
@@ -171,7 +156,8 @@ struct Walker : Ctx<STORE, COUNT> {
                     float t = dd > 0.0f ? (ceilf(o) - o) / dd : (floorf(o) - o) / dd;
                     hit = add(a.old_o, scl(t, a.ds));
                 }
-                h.lit = lighting(col, n, rwp, hit);
+                h.col = col;
+                h.n = n;
                 h.so = hit;
                 h.region = cr;
                 h.longest = true;
@@ -185,7 +171,7 @@ struct Walker : Ctx<STORE, COUNT> {
     // rayMarchVoxelGridLongestAxis (Renderer.cuh:760-915) /
     // shadowRayMarchVoxelGridLongestAxis (:495-631).
     template <bool SHADOW>
-    __device__ bool grid_longest(f3& oo, f3 od, uint32_t reg, f3 rwp, i3 cr, Hit& h) {
+    __device__ bool grid_longest(f3& oo, f3 od, uint32_t reg, i3 cr, Hit& h) {
         LA a;
         // Ray::convertRayToLongestAxisDirection (Ray.cuh:19-71)
         float ax = fabsf(od.x), ay = fabsf(od.y), az = fabsf(od.z), k;
@@ -220,22 +206,22 @@ struct Walker : Ctx<STORE, COUNT> {
                 float sp = comp(a.old_o, a.S) + comp(a.ds, a.S) * t1;
                 int32_t sd = f2i(floorf(sp)) - geti(a.g, a.S);
                 uint32_t a0 = sd != 0 ? a.S : a.M, a1 = sd != 0 ? a.M : a.S;
-                r = axis_step<SHADOW>(oo, a, a0, false, reg, rwp, cr, h, res);
+                r = axis_step<SHADOW>(oo, a, a0, false, reg, cr, h, res);
                 if (r == 1) return res;
                 if (r == 2) continue;
-                r = axis_step<SHADOW>(oo, a, a1, false, reg, rwp, cr, h, res);
+                r = axis_step<SHADOW>(oo, a, a1, false, reg, cr, h, res);
                 if (r == 1) return res;
                 if (r == 2) continue;
             } else if (adM != 0) {
-                r = axis_step<SHADOW>(oo, a, a.M, false, reg, rwp, cr, h, res);
+                r = axis_step<SHADOW>(oo, a, a.M, false, reg, cr, h, res);
                 if (r == 1) return res;
                 if (r == 2) continue;
             } else if (adS != 0) {
-                r = axis_step<SHADOW>(oo, a, a.S, false, reg, rwp, cr, h, res);
+                r = axis_step<SHADOW>(oo, a, a.S, false, reg, cr, h, res);
                 if (r == 1) return res;
                 if (r == 2) continue;
             }
-            r = axis_step<SHADOW>(oo, a, a.L, true, reg, rwp, cr, h, res);
+            r = axis_step<SHADOW>(oo, a, a.L, true, reg, cr, h, res);
             if (r == 1) return res;
             if (r == 2) continue;
             a.old_o = a.ray_o;
@@ -244,7 +230,7 @@ struct Walker : Ctx<STORE, COUNT> {
             seti(a.ad, a.S, f2i(comp(a.ray_o, a.S)) - geti(a.g, a.S));
         }
         oo = a.old_o;     // Renderer.cuh:912 (direction of originalRay kept)
-        return grid_original<SHADOW>(oo, od, reg, rwp, cr, h);
+        return grid_original<SHADOW>(oo, od, reg, cr, h);
     }
 
     // rayMarchVoxelScene (Renderer.cuh:338-434) / rayMarchVoxelSceneLongestAxis (:917-1010).
@@ -277,9 +263,8 @@ struct Walker : Ctx<STORE, COUNT> {
                 if (!tick()) return false;
                 if (!this->template skip_null<false>(cr, o, d, reg)) return false;
             }
-            f3 rwp = add(tr, mk((float)(cr.x * kBlock), (float)(cr.y * kBlock), (float)(cr.z * kBlock)));
-            bool hit = ALGO == ALGO_ORIGINAL ? grid_original<false>(o, d, reg, rwp, cr, h)
-                                             : grid_longest<false>(o, d, reg, rwp, cr, h);
+            bool hit = ALGO == ALGO_ORIGINAL ? grid_original<false>(o, d, reg, cr, h)
+                                             : grid_longest<false>(o, d, reg, cr, h);
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
@@ -300,8 +285,8 @@ struct Walker : Ctx<STORE, COUNT> {
                 if (!tick()) return false;
                 if (!this->template skip_null<!LONGEST>(cr, o, d, reg)) return false;
             }
-            bool hit = LONGEST ? grid_longest<true>(o, d, reg, mk(0.0f, 0.0f, 0.0f), cr, dummy)
-                               : grid_original<true>(o, d, reg, mk(0.0f, 0.0f, 0.0f), cr, dummy);
+            bool hit = LONGEST ? grid_longest<true>(o, d, reg, cr, dummy)
+                               : grid_original<true>(o, d, reg, cr, dummy);
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
@@ -331,9 +316,13 @@ __global__ __launch_bounds__(256) void march_kernel(KScene s, KView v) {
             Hit h;
             if (w.template primary<ALGO>(ro, rd, h)) {
                 bool sh = false;
+                // applyLighting (Renderer.cuh:249-258) at the hit; regionWorldPosition (:413)
+                const f3 rwp = add(ld3(v.translation), mk((float)(h.region.x * kBlock), (float)(h.region.y * kBlock),
+                                                          (float)(h.region.z * kBlock)));
+                const uint32_t lit = w.lighting(h.col, h.n, rwp, h.so);
                 if (v.use_shadows)
                     sh = h.longest ? w.template shadow<true>(h.so, h.region) : w.template shadow<false>(h.so, h.region);
-                col = h.lit * (uint32_t)!sh;
+                col = lit * (uint32_t)!sh;
             }
             if (w.aborted) col = 0;
             bytes = w.bytes + 4u;                 // + the pixel write
