@@ -82,8 +82,19 @@ __device__ __forceinline__ uint32_t hash2(uint32_t k, uint32_t prime) {
     return k;
 }
 
-typedef uint2 Blk;    // VCS directory entry {block offset (16-B units), n}
-__device__ __forceinline__ bool absent(Blk b) { return b.x == kNone; }
+// Fill the workgroup's 256-entry table of (float)c / 255.0f (correctly rounded
+// division, same as VoxelFunctions.cuh:71-73) -- all threads must call it.
+__device__ __forceinline__ const float* load_inv255(float* lds) {
+    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) lds[i] = (float)i / 255.0f;
+    __syncthreads();
+    return lds;
+}
+
+// VCS: the mask word of the cluster holding the voxel, {occupancy bits,
+// value index of the word's first voxel} or {0, kNone} (no cluster).
+// Hashtable: unused ({0,0}: the space always exists).
+typedef uint2 Blk;
+__device__ __forceinline__ bool absent(Blk b) { return b.y == kNone; }
 
 struct Hit {
     uint32_t col;       // the voxel's stored colour
@@ -96,6 +107,7 @@ struct Hit {
 template <int STORE, bool COUNT>
 struct Ctx {
     const KScene& s;
+    const float* inv255 = nullptr;   // LDS table c / 255.0f, c in [0,255] (see load_inv255)
     const KView& v;
     uint32_t iters = 0;
     bool aborted = false;
@@ -124,25 +136,43 @@ struct Ctx {
         return s.region_slot[ux + uy * s.D + uz * s.D * s.D];
     }
 
+    // `short` getVoxelClusterID (VoxelClusterStore.cuh:21-24); -1 = past the
+    // reference's 512-entry directory (no cluster).
+    __device__ __forceinline__ static int32_t cluster_id(int32_t x, int32_t y, int32_t z) {
+        uint32_t c = (((uint32_t)x >> 3) << 6) | (((uint32_t)y >> 3) << 3) | ((uint32_t)z >> 3);
+        int32_t cid = (int32_t)(int16_t)(uint16_t)c;
+        return cid < 512 ? cid : -1;
+    }
+    // In-cluster voxel index ((x&7)<<6|(y&7)<<3|z&7): same order as the
+    // reference's full keys x<<20|y<<10|z inside one cluster.
+    __device__ __forceinline__ static uint32_t in_cluster(int32_t x, int32_t y, int32_t z) {
+        return (((uint32_t)x & 7u) << 6) | (((uint32_t)y & 7u) << 3) | ((uint32_t)z & 7u);
+    }
+    __device__ __forceinline__ const uint2* masks(uint32_t reg, int32_t cid) const {
+        return s.vcs_mask + ((size_t)(reg * 512u + (uint32_t)cid) << 4);
+    }
+
     // doesVoxelSpaceExist (StorageStructure.cuh:29-32,49-52) ->
     // VoxelClusterStore::doesClusterExist (VoxelClusterStore.cuh:93-99).
-    // Returns the directory entry {block offset, n} (VCS) or {0,0} (hashtable:
-    // the space always exists); absent() = no cluster.
+    // VCS: one 8-B read of the mask word the later lookup of this voxel needs,
+    // so existence and lookup share a single dependent load.
     __device__ __forceinline__ Blk exists(uint32_t reg, int32_t x, int32_t y, int32_t z) {
         if (STORE == STORE_HASH) return Blk{0u, 0u};
         count(4);
-        uint32_t c = (((uint32_t)x >> 3) << 6) | (((uint32_t)y >> 3) << 3) | ((uint32_t)z >> 3);
-        int32_t cid = (int32_t)(int16_t)(uint16_t)c;      // `short` getVoxelClusterID
-        if (cid < 0 || cid >= 512) return Blk{kNone, 0u}; // past the reference's directory
-        return s.vcs_dir[reg * 512u + (uint32_t)cid];
+        const int32_t cid = cluster_id(x, y, z);
+        if (cid < 0) return Blk{0u, kNone};
+        return masks(reg, cid)[in_cluster(x, y, z) >> 5];
     }
 
     // Reference binary-search probes for a key of rank `rank` (number of keys
     // < q) among n sorted keys: key[mid] < q <=> mid < rank, key[mid] == q <=>
     // found && mid == rank (performBinarySearch, VoxelClusterStore.cuh:101-126).
-    // Only the COUNT instantiations evaluate it (SURVEY 8(d) bytes).
-    __device__ __forceinline__ void count_bsearch(uint32_t n, uint32_t rank, bool found) {
+    // Only the COUNT instantiations evaluate it (SURVEY 8(d) bytes); n and the
+    // rank come from the cluster's first and last mask words.
+    __device__ __forceinline__ void count_bsearch(const uint2* m, uint32_t idx, bool found) {
         if (!COUNT) return;
+        const uint2 m0 = m[0], m15 = m[15];
+        const uint32_t n = m15.y + __popc(m15.x) - m0.y, rank = idx - m0.y;
         int32_t low = 0, high = (int32_t)n - 1;
         uint32_t probes = 0;
         while (low <= high) {
@@ -155,84 +185,62 @@ struct Ctx {
     }
 
     // A coordinate outside [0,64) whose `short` cluster id still lands in the
-    // directory (longest-axis walks can probe one): the reference binary-searches
-    // the full key x<<20|y<<10|z, which no key of the block can equal.  Rare;
-    // run the reference search verbatim over the block's keys widened back to
-    // full keys, so the probe count (COUNT) is exact too.
-    __device__ uint32_t lookup_aliased(const uint4* b, VcsGeom gm, uint32_t n, int32_t x,
-                                                                 int32_t y, int32_t z) {
-        const uint32_t ux = (uint32_t)x, uy = (uint32_t)y, uz = (uint32_t)z;
-        const uint32_t K = (ux << 20) | (uy << 10) | uz;
-        const uint32_t c = (((ux >> 3) << 6) | ((uy >> 3) << 3) | (uz >> 3)) & 0x1FFu;
-        const uint32_t bx = (c >> 6) * 8u, by = ((c >> 3) & 7u) * 8u, bz = (c & 7u) * 8u;
-        const uint16_t* k16 = reinterpret_cast<const uint16_t*>(b + gm.u_keys);
-        count(4);
-        int32_t low = 0, high = (int32_t)n - 1;
-        while (low <= high) {
-            int32_t mid = low + ((high - low) >> 1);
-            const uint32_t c9 = k16[mid];
-            const uint32_t full = ((bx + (c9 >> 6)) << 20) | ((by + ((c9 >> 3) & 7u)) << 10) | (bz + (c9 & 7u));
-            count(4);
-            if (full == K) { count(4); return reinterpret_cast<const uint32_t*>(b + gm.u_vals)[mid]; }
-            if (full < K) low = mid + 1; else high = mid - 1;
+    // directory (very large longest-axis grid coordinates): the reference
+    // binary-searches the 32-bit key x<<20|y<<10|z (which wraps) among the
+    // cluster's full keys.  Those are increasing in the in-cluster index, so the
+    // number of keys below K is the population below the first index t whose
+    // full key is >= K (found iff that key equals K and is present).  Exact, rare.
+    __device__ __forceinline__ uint32_t lookup_aliased(uint32_t reg, int32_t x, int32_t y, int32_t z) {
+        const int32_t cid = cluster_id(x, y, z);
+        const uint2* m = masks(reg, cid);
+        const uint32_t K = ((uint32_t)x << 20) | ((uint32_t)y << 10) | (uint32_t)z;
+        const uint32_t bx = ((uint32_t)cid >> 6) * 8u, by = (((uint32_t)cid >> 3) & 7u) * 8u, bz = ((uint32_t)cid & 7u) * 8u;
+        auto full = [&](uint32_t q) { return ((bx + (q >> 6)) << 20) | ((by + ((q >> 3) & 7u)) << 10) | (bz + (q & 7u)); };
+        uint32_t lo = 0, hi = 512;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (full(mid) < K) lo = mid + 1; else hi = mid;
         }
-        return kEmpty;
-    }
-
-    // Number of the 8 16-bit keys of a node that are < q.
-    __device__ __forceinline__ static uint32_t count_lt(uint4 nd, uint32_t q) {
-        uint32_t c = 0;
-        c += (nd.x & 0xFFFFu) < q; c += (nd.x >> 16) < q;
-        c += (nd.y & 0xFFFFu) < q; c += (nd.y >> 16) < q;
-        c += (nd.z & 0xFFFFu) < q; c += (nd.z >> 16) < q;
-        c += (nd.w & 0xFFFFu) < q; c += (nd.w >> 16) < q;
-        return c;
-    }
-    __device__ __forceinline__ static uint32_t key_at(uint4 nd, uint32_t j) {
-        uint32_t w = j < 4u ? (j < 2u ? nd.x : nd.y) : (j < 6u ? nd.z : nd.w);
-        return (j & 1u) ? (w >> 16) : (w & 0xFFFFu);
+        if (lo == 512u) {
+            const uint2 m15 = m[15];
+            count_bsearch(m, m15.y + __popc(m15.x), false);
+            return kEmpty;
+        }
+        const uint2 w = m[lo >> 5];
+        const uint32_t bit = lo & 31u;
+        const bool found = full(lo) == K && ((w.x >> bit) & 1u);
+        const uint32_t idx = w.y + __popc(w.x & ((1u << bit) - 1u));
+        count_bsearch(m, idx, found);
+        return found ? s.vcs_vals[idx] : kEmpty;
     }
 
     // VoxelClusterStore::lookupVoxel / performBinarySearch (VoxelClusterStore.cuh:101-135):
-    // the same search over the cluster's sorted keys, widened to one 16-B node
-    // of 8 keys per level (9-ary): 1 node load for n <= 8, 2 for n <= 64, 3 for
-    // n <= 512 instead of 1 + ~log2(n) dependent word loads.  Identical result.
-    // CuckooHashTable::lookupVoxel (CuckooHashTable.cuh:59-76).
+    // the binary search's answer (is the key present, and its value) read off
+    // the cluster's occupancy mask: bit q of the mask word `blk` fetched by
+    // exists(), value index = word base + popcount of the lower bits.  No
+    // further dependent load before the value itself.
+    // CuckooHashTable::lookupVoxel (CuckooHashTable.cuh:59-76): both candidate
+    // slots are requested together (the second read is counted only when the
+    // reference would make it).
     __device__ __forceinline__ uint32_t lookup(uint32_t reg, Blk blk, int32_t x, int32_t y, int32_t z) {
         if (STORE == STORE_VCS) {
-            const uint32_t n = blk.y;
-            const VcsGeom gm = vcs_geom(n);
-            const uint4* b = s.vcs_pool + blk.x;
-            if (((uint32_t)x | (uint32_t)y | (uint32_t)z) >= 64u) return lookup_aliased(b, gm, n, x, y, z);
-            const uint32_t q = (((uint32_t)x & 7u) << 6) | (((uint32_t)y & 7u) << 3) | ((uint32_t)z & 7u);
-            uint32_t grp = 0, chunk = 0;
-            if (gm.groups > 1u) {
-                grp = count_lt(b[0], q);
-                if (grp >= gm.groups) { count_bsearch(n, n, false); return kEmpty; }
-            }
-            if (gm.chunks > 1u) {
-                const uint32_t cl = count_lt(b[gm.u_f1 + grp], q);
-                const uint32_t in_grp = min(8u, gm.chunks - 8u * grp);
-                if (cl >= in_grp) { count_bsearch(n, n, false); return kEmpty; }
-                chunk = 8u * grp + cl;
-            }
-            const uint4 leaf = b[gm.u_keys + chunk];
-            const uint32_t r = count_lt(leaf, q);
-            const bool found = r < 8u && key_at(leaf, r) == q;
-            count_bsearch(n, min(8u * chunk + r, n), found);
-            if (!found) return kEmpty;
-            return reinterpret_cast<const uint32_t*>(b + gm.u_vals)[8u * chunk + r];
+            if (((uint32_t)x | (uint32_t)y | (uint32_t)z) >= 64u) return lookup_aliased(reg, x, y, z);
+            const uint32_t bit = in_cluster(x, y, z) & 31u;
+            const bool found = (blk.x >> bit) & 1u;
+            const uint32_t idx = blk.y + __popc(blk.x & ((1u << bit) - 1u));
+            if (COUNT) count_bsearch(masks(reg, cluster_id(x, y, z)), idx, found);
+            return found ? s.vcs_vals[idx] : kEmpty;
         } else {
             const uint32_t key = ((uint32_t)x << 20) | ((uint32_t)y << 10) | (uint32_t)z;   // generate3DPoint
-            uint4 m = s.ht_meta[reg];          // {base, M, prime, offset}
-            uint32_t s1 = hash1(key, m.w) % m.y;
+            const uint4 m = s.ht_meta[reg];          // {base, M, prime, offset}
+            const uint32_t s1 = hash1(key, m.w) % m.y;
+            const uint32_t s2 = hash2(key, m.z) % m.y;
+            const uint2 e1 = s.ht_slots[m.x + s1];
+            const uint2 e2 = s.ht_slots[m.x + m.y + s2];
             count(4);
-            uint2 e = s.ht_slots[m.x + s1];
-            if (e.x == key) { count(4); return e.y; }
-            uint32_t s2 = hash2(key, m.z) % m.y;
+            if (e1.x == key) { count(4); return e1.y; }
             count(4);
-            e = s.ht_slots[m.x + m.y + s2];
-            if (e.x == key) { count(4); return e.y; }
+            if (e2.x == key) { count(4); return e2.y; }
             return kEmpty;
         }
     }
@@ -241,7 +249,9 @@ struct Ctx {
     // (Renderer.cuh:57-86,249-258), colour packing (VoxelFunctions.cuh:69-83).
     __device__ __forceinline__ uint32_t lighting(uint32_t col, f3 n, f3 rwp, f3 ro) const {
         f3 LC = ld3(v.LC);
-        f3 c = mk((float)(col >> 16) / 255.0f, (float)((col >> 8) & 0xFFu) / 255.0f, (float)(col & 0xFFu) / 255.0f);
+        // convertRGBIntegerColorToVector: c / 255.0f per channel, read from the exact
+        // (correctly rounded) LDS table; colours are < 2^24 so R = col >> 16 <= 255.
+        f3 c = mk(inv255[col >> 16], inv255[(col >> 8) & 0xFFu], inv255[col & 0xFFu]);
         f3 r;
         if (v.use_point_light) {
             f3 p2l = sub(ld3(v.LP), add(rwp, ro));

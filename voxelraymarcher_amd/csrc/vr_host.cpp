@@ -135,9 +135,9 @@ struct vr_scene {
     int32_t min_coord = 0;
     uint32_t n_regions = 0;
     uint64_t n_voxels = 0;
-    DevBuf region_slot, vcs_dir, vcs_pool, ht_meta, ht_slots;
+    DevBuf region_slot, vcs_mask, vcs_vals, ht_meta, ht_slots;
     uint64_t device_bytes() const {
-        return region_slot.bytes + vcs_dir.bytes + vcs_pool.bytes + ht_meta.bytes + ht_slots.bytes;
+        return region_slot.bytes + vcs_mask.bytes + vcs_vals.bytes + ht_meta.bytes + ht_slots.bytes;
     }
 };
 
@@ -157,7 +157,7 @@ struct DeviceGuard {
 
 void free_scene(vr_scene* s) {
     if (!s) return;
-    DevBuf* bufs[] = {&s->region_slot, &s->vcs_dir, &s->vcs_pool, &s->ht_meta, &s->ht_slots};
+    DevBuf* bufs[] = {&s->region_slot, &s->vcs_mask, &s->vcs_vals, &s->ht_meta, &s->ht_slots};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     delete s;
@@ -248,69 +248,54 @@ int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* 
     if (rc_up) { free_scene(s); return rc_up; }
 
     if (store == VR_STORE_VCS) {
-        // VoxelClusterStore ctor (VoxelClusterStore.cuh:37-85): per region a
-        // 512-entry directory and, per non-empty cluster, its keys in ascending
-        // order -- stored as 16-bit in-cluster indices (same order as the full
-        // keys inside one cluster) in a static 9-ary tree of 16-B nodes, then
-        // the values (vr_internal.h "VCS").
-        std::vector<uint2> dir((size_t)nr * 512, uint2{vr::kNone, 0u});
-        std::vector<uint32_t> pool;   // 4 words per 16-B unit
-        pool.reserve(2 * m + 4096);
-        std::vector<uint32_t> cid_of;
-        std::vector<uint32_t> order;
+        // VoxelClusterStore ctor (VoxelClusterStore.cuh:37-85): per region 512
+        // cluster slots; a cluster's sorted keys become a 512-bit occupancy
+        // mask over in-cluster indices (same order) with a running value index
+        // per 32-bit word, its values follow in key order (vr_internal.h "VCS").
+        if ((uint64_t)nr * 512u * 16u * sizeof(uint2) > (1ull << 40)) { free_scene(s); return fail(VR_E_BUILD, "VCS mask table too large"); }
+        std::vector<uint2> mask((size_t)nr * 512 * 16, uint2{0u, vr::kNone});
+        std::vector<uint32_t> vals;
+        vals.reserve(m);
         for (uint32_t r = 0; r < nr; ++r) {
             size_t b = region_begin[r], e = region_begin[r + 1];
-            uint32_t counts[512] = {0}, first[513];
-            cid_of.resize(e - b);
+            uint32_t bits[512][16];
+            uint32_t cnt[512] = {0};
+            memset(bits, 0, sizeof bits);
             for (size_t i = b; i < e; ++i) {
                 uint32_t key = (uint32_t)recs[i].k;
                 uint32_t x = key >> 20, y = (key >> 10) & 0x3FFu, z = key & 0x3FFu;
                 uint32_t c = ((x / 8u) << 6) | ((y / 8u) << 3) | (z / 8u);
-                cid_of[i - b] = c;
-                counts[c]++;
+                uint32_t q = ((x & 7u) << 6) | ((y & 7u) << 3) | (z & 7u);
+                bits[c][q >> 5] |= 1u << (q & 31u);
+                cnt[c]++;
             }
-            first[0] = 0;
-            for (uint32_t c = 0; c < 512; ++c) first[c + 1] = first[c] + counts[c];
-            order.assign(e - b, 0);
+            // values: cluster by cluster, each in key order (keys arrive ascending
+            // within a region, and one cluster's keys ascend with q)
+            uint32_t start[512];
+            uint32_t acc = (uint32_t)vals.size();
+            for (uint32_t c = 0; c < 512; ++c) { start[c] = acc; acc += cnt[c]; }
+            vals.resize(acc);
             uint32_t fill[512] = {0};
-            for (size_t i = b; i < e; ++i) {      // keys arrive ascending: stable bucket keeps them sorted
-                uint32_t c = cid_of[i - b];
-                order[first[c] + fill[c]++] = (uint32_t)(i - b);
+            for (size_t i = b; i < e; ++i) {
+                uint32_t key = (uint32_t)recs[i].k;
+                uint32_t x = key >> 20, y = (key >> 10) & 0x3FFu, z = key & 0x3FFu;
+                uint32_t c = ((x / 8u) << 6) | ((y / 8u) << 3) | (z / 8u);
+                vals[start[c] + fill[c]++] = recs[i].val;
             }
             for (uint32_t c = 0; c < 512; ++c) {
-                const uint32_t n = counts[c];
-                if (!n) continue;
-                const vr::VcsGeom gm = vr::vcs_geom(n);
-                if (pool.size() / 4 + gm.units >= 0xFFFFFFFFull) { free_scene(s); return fail(VR_E_BUILD, "VCS pool exceeds 32-bit offsets"); }
-                const size_t base = pool.size();
-                dir[(size_t)r * 512 + c] = uint2{(uint32_t)(base / 4), n};
-                pool.resize(base + 4 * (size_t)gm.units, 0u);
-                uint16_t* k16 = reinterpret_cast<uint16_t*>(pool.data() + base);
-                uint32_t* vals = pool.data() + base + 4 * (size_t)gm.u_vals;
-                std::vector<uint16_t> keys(8 * (size_t)gm.chunks, 0xFFFFu);
-                for (uint32_t j = 0; j < n; ++j) {
-                    const Rec& rc = recs[b + order[first[c] + j]];
-                    uint32_t key = (uint32_t)rc.k;
-                    uint32_t x = key >> 20, y = (key >> 10) & 0x3FFu, z = key & 0x3FFu;
-                    keys[j] = (uint16_t)(((x & 7u) << 6) | ((y & 7u) << 3) | (z & 7u));
-                    vals[j] = rc.val;
+                if (!cnt[c]) continue;
+                uint2* w = &mask[((size_t)r * 512 + c) * 16];
+                uint32_t run = start[c];
+                for (uint32_t j = 0; j < 16; ++j) {
+                    w[j] = uint2{bits[c][j], run};
+                    run += (uint32_t)__builtin_popcount(bits[c][j]);
                 }
-                auto chunk_max = [&](uint32_t ch) { return keys[std::min<size_t>(8 * (size_t)ch + 7, n - 1)]; };
-                if (gm.groups > 1)                 // F0: max key of each 64-key group
-                    for (uint32_t g = 0; g < 8; ++g)
-                        k16[g] = g < gm.groups ? keys[std::min<size_t>(64 * (size_t)g + 63, n - 1)] : 0xFFFFu;
-                if (gm.chunks > 1)                 // F1: max key of each chunk, one node per group
-                    for (uint32_t g = 0; g < gm.groups; ++g)
-                        for (uint32_t j = 0; j < 8; ++j) {
-                            uint32_t ch = 8 * g + j;
-                            k16[8 * (gm.u_f1 + g) + j] = ch < gm.chunks ? chunk_max(ch) : 0xFFFFu;
-                        }
-                for (size_t j = 0; j < keys.size(); ++j) k16[8 * (size_t)gm.u_keys + j] = keys[j];
             }
         }
-        if (pool.empty()) pool.assign(4, 0u);
-        if ((rc_up = upload(s->vcs_dir, dir.data(), dir.size() * sizeof(uint2))) ||
-            (rc_up = upload(s->vcs_pool, pool.data(), pool.size() * 4))) {
+        if (mask.empty()) mask.assign(16, uint2{0u, vr::kNone});
+        if (vals.empty()) vals.assign(1, 0u);
+        if ((rc_up = upload(s->vcs_mask, mask.data(), mask.size() * sizeof(uint2))) ||
+            (rc_up = upload(s->vcs_vals, vals.data(), vals.size() * 4))) {
             free_scene(s);
             return rc_up;
         }
@@ -350,8 +335,8 @@ int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* 
 vr::KScene kscene(const vr_scene* s) {
     vr::KScene k{};
     k.region_slot = (const uint32_t*)s->region_slot.p;
-    k.vcs_dir = (const uint2*)s->vcs_dir.p;
-    k.vcs_pool = (const uint4*)s->vcs_pool.p;
+    k.vcs_mask = (const uint2*)s->vcs_mask.p;
+    k.vcs_vals = (const uint32_t*)s->vcs_vals.p;
     k.ht_meta = (const uint4*)s->ht_meta.p;
     k.ht_slots = (const uint2*)s->ht_slots.p;
     k.D = s->D;

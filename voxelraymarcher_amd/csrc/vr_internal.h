@@ -14,23 +14,21 @@ constexpr uint32_t kIterBudget = 65536u;     // per-pixel hang guard
 
 // Device view of one immutable scene.  All offsets are 32-bit word indices.
 //  region_slot[D^3]          : region index r, or kNone (null StorageStructure*)
-//  VCS   : vcs_dir[r*512+cid]: {block offset in 16-B units, n} or {kNone, 0}
-//                              (VoxelClusterStore::deviceBlockMemAddress + the block's count)
-//          vcs_pool block    : the cluster's keys ascending (VoxelClusterStore.cuh:61-76) as
-//                              16-bit in-cluster indices ((x&7)<<6|(y&7)<<3|z&7, same order),
-//                              laid out as a static 9-ary search tree of 16-B nodes:
-//                                [F0: max key of each 64-key group]   (only if n > 64)
-//                                [F1: max key of each 8-key chunk, one node per group] (n > 8)
-//                                [chunks: 8 keys per node, padded with 0xFFFF]
-//                                [values: n uint32, key order]
-//                              see vcs_block_units() / Ctx::lookup.
+//  VCS   : vcs_mask[((r*512+cid)*16 + w]  (one 128-B record per cluster slot of an
+//                              occupied region; VoxelClusterStore::deviceBlockMemAddress
+//                              + the cluster's sorted keys, VoxelClusterStore.cuh:37-85)
+//                              {bits, index}: bit b set <=> the voxel with in-cluster index
+//                              q = 32w+b ((x&7)<<6|(y&7)<<3|z&7, the keys' order) is stored;
+//                              index = vcs_vals position of the word's first stored voxel.
+//                              Absent cluster: {0, kNone} in all 16 words.
+//          vcs_vals[]        : colours, cluster by cluster in key order.
 //  Cuckoo: ht_meta[r]        : {base, M, prime, offset}
 //          ht_slots[base+i]  : table 1 slot i {key, value};
 //          ht_slots[base+M+i]: table 2 slot i {key, value}; empty key = kEmpty
 struct KScene {
     const uint32_t* region_slot;
-    const uint2* vcs_dir;
-    const uint4* vcs_pool;
+    const uint2* vcs_mask;
+    const uint32_t* vcs_vals;
     const uint4* ht_meta;
     const uint2* ht_slots;
     uint32_t D;
@@ -52,21 +50,6 @@ struct KView {
     uint32_t* out;
     unsigned long long* bytes;
 };
-
-// VCS block geometry in 16-B units for a cluster of n keys (n >= 1).
-struct VcsGeom {
-    uint32_t groups, chunks, u_f1, u_keys, u_vals, units;
-};
-__host__ __device__ inline VcsGeom vcs_geom(uint32_t n) {
-    VcsGeom g;
-    g.groups = (n + 63u) >> 6;
-    g.chunks = (n + 7u) >> 3;
-    g.u_f1 = g.groups > 1u ? 1u : 0u;
-    g.u_keys = g.u_f1 + (g.chunks > 1u ? g.groups : 0u);
-    g.u_vals = g.u_keys + g.chunks;
-    g.units = g.u_vals + ((n + 3u) >> 2);
-    return g;
-}
 
 // Launch one render (defined in vr_march.hip).
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,

@@ -37,7 +37,7 @@ struct Walker : Ctx<STORE, COUNT> {
     // iteration instead of two divergent ones.  Lighting is applied by the
     // caller after the walk (Hit carries colour, normal and position).
     template <bool SHADOW>
-    __device__ bool grid_original(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h) {
+    __device__ __forceinline__ bool grid_original(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h) {
         const bool px = d.x > 0.0f, py = d.y > 0.0f, pz = d.z > 0.0f;
         const bool zx = SHADOW && d.x == 0.0f, zy = SHADOW && d.y == 0.0f, zz = SHADOW && d.z == 0.0f;
         float nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
@@ -48,6 +48,11 @@ struct Walker : Ctx<STORE, COUNT> {
         float tZ = zz ? kInf : (nZ - o.z) / d.z;
         float tMin = fminf(tX, fminf(tY, tZ));
         o = add(o, scl(tMin + kEps, d));
+        // Software-pipelined: the step for this voxel is computed before its
+        // lookup, and the directory entry of the next voxel is requested
+        // before this voxel's search chain, so the two latencies overlap.  On
+        // a hit the precomputed step is discarded; the look-ahead directory
+        // read is counted only when its iteration runs.
         uint32_t col = kEmpty;
         while (in_region(o)) {
             if (!tick()) return false;
@@ -92,7 +97,7 @@ struct Walker : Ctx<STORE, COUNT> {
     // performVoxelSpaceJump (Renderer.cuh:696-751) / performShadowVoxelSpaceJump (:441-492).
     // Returns 0 = EMPTY_VAL (left region / aborted), 1 = hit, 2 = CONTINUE_VAL.
     template <bool SHADOW>
-    __device__ int jump(f3& oo, LA& a, uint32_t reg, i3 cr, Hit& h) {
+    __device__ __forceinline__ int jump(f3& oo, LA& a, uint32_t reg, i3 cr, Hit& h) {
         float tX = 0.0f, tY = 0.0f, tZ = 0.0f, tMin = 0.0f;
         Blk blk;
         while (absent(blk = exists(reg, a.g.x, a.g.y, a.g.z))) {
@@ -133,7 +138,7 @@ struct Walker : Ctx<STORE, COUNT> {
     // One "grid += diff; exists? else jump; lookup; hit" block
     // (Renderer.cuh:807-901 / :542-617).  0 = go on, 1 = return *res, 2 = continue.
     template <bool SHADOW>
-    __device__ int axis_step(f3& oo, LA& a, uint32_t axis, bool long_axis, uint32_t reg, i3 cr,
+    __device__ __forceinline__ int axis_step(f3& oo, LA& a, uint32_t axis, bool long_axis, uint32_t reg, i3 cr,
                              Hit& h, bool& res) {
         seti(a.g, axis, geti(a.g, axis) + geti(a.ad, axis));
         Blk blk = exists(reg, a.g.x, a.g.y, a.g.z);
@@ -171,7 +176,7 @@ struct Walker : Ctx<STORE, COUNT> {
     // rayMarchVoxelGridLongestAxis (Renderer.cuh:760-915) /
     // shadowRayMarchVoxelGridLongestAxis (:495-631).
     template <bool SHADOW>
-    __device__ bool grid_longest(f3& oo, f3 od, uint32_t reg, i3 cr, Hit& h) {
+    __device__ __forceinline__ bool grid_longest(f3& oo, f3 od, uint32_t reg, i3 cr, Hit& h) {
         LA a;
         // Ray::convertRayToLongestAxisDirection (Ray.cuh:19-71)
         float ax = fabsf(od.x), ay = fabsf(od.y), az = fabsf(od.z), k;
@@ -235,7 +240,7 @@ struct Walker : Ctx<STORE, COUNT> {
 
     // rayMarchVoxelScene (Renderer.cuh:338-434) / rayMarchVoxelSceneLongestAxis (:917-1010).
     template <int ALGO>
-    __device__ bool primary(f3 wo, f3 wd, Hit& h) {
+    __device__ __forceinline__ bool primary(f3 wo, f3 wd, Hit& h) {
         f3 tr = ld3(v.translation);
         f3 so = scl(v.scale_f, sub(wo, tr));      // Ray::convertRayToLocalSpace (Ray.cuh:14-17)
         f3 d = wd;
@@ -275,7 +280,7 @@ struct Walker : Ctx<STORE, COUNT> {
     // isInShadowOriginalRayMarch (Renderer.cuh:174-235) /
     // isInShadowRayMarchVoxelSceneLongestAxis (:633-694).
     template <bool LONGEST>
-    __device__ bool shadow(f3 o, i3 cr) {
+    __device__ __forceinline__ bool shadow(f3 o, i3 cr) {
         f3 d = ld3(v.L);
         Hit dummy;
         while (in_scene(cr)) {
@@ -297,7 +302,9 @@ struct Walker : Ctx<STORE, COUNT> {
 
 // rayMarchSceneOriginal / rayMarchSceneJumpAxis (Renderer.cuh:1033-1063).
 template <int STORE, int ALGO, bool COUNT>
-__global__ __launch_bounds__(256) void march_kernel(KScene s, KView v) {
+__global__ __launch_bounds__(256, ALGO == ALGO_ORIGINAL ? 7 : 3) void march_kernel(KScene s, KView v) {
+    __shared__ float inv255_lds[256];
+    const float* inv255 = load_inv255(inv255_lds);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t x = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
     const uint32_t l = (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
@@ -313,6 +320,7 @@ __global__ __launch_bounds__(256) void march_kernel(KScene s, KView v) {
             f3 ro = add(add(ld3(v.llc), scl(u, ld3(v.hor))), scl(vv, ld3(v.ver)));
             f3 rd = unit(sub(ro, ld3(v.org)));
             Walker<STORE, COUNT> w(s, v);
+            w.inv255 = inv255;
             Hit h;
             if (w.template primary<ALGO>(ro, rd, h)) {
                 bool sh = false;

@@ -171,7 +171,9 @@ struct Machine : Ctx<STORE, COUNT> {
         return 0;
     }
 
-    // P_DDA: one iteration of the original DDA loop.
+    // P_DDA: one iteration of the original DDA loop; the cluster skip
+    // (:290-306) and the voxel step (:318-331) share one select-driven step
+    // (see vr_march.hip grid_original).
     __device__ int dda_step() {
         if (!in_region(o)) {              // loop exit -> back in the region loop (:421-429)
             advance_region(cr, o);
@@ -180,33 +182,25 @@ struct Machine : Ctx<STORE, COUNT> {
         }
         if (!tick()) return finish(0);
         const bool gd = shadow;
-        int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-        Blk blk = exists(reg, vx, vy, vz);
-        if (absent(blk)) {               // cluster skip (:290-306), block-scoped t values
-            int32_t cx = d.x > 0.0f ? ((vx / 8) + 1) * 8 : (vx / 8) * 8;
-            int32_t cy = d.y > 0.0f ? ((vy / 8) + 1) * 8 : (vy / 8) * 8;
-            int32_t cz = d.z > 0.0f ? ((vz / 8) + 1) * 8 : (vz / 8) * 8;
-            float sX = gdiv((float)cx, o.x, d.x, gd);
-            float sY = gdiv((float)cy, o.y, d.y, gd);
-            float sZ = gdiv((float)cz, o.z, d.z, gd);
-            float sMin = fminf(sX, fminf(sY, sZ));
-            o = add(o, scl(sMin + kEps, d));
-            return 0;
+        const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
+        const Blk blk = exists(reg, vx, vy, vz);
+        const bool skip = absent(blk);
+        if (!skip) {
+            const uint32_t col = lookup(reg, blk, vx, vy, vz);
+            if (col != kEmpty) {
+                if (shadow) return finish(0);
+                lit = lighting(col, normal_from_t(tX, tY, tZ, tMin, d), rwp(), o);
+                return start_shadow(o, false);
+            }
         }
-        uint32_t col = lookup(reg, blk, vx, vy, vz);
-        if (col != kEmpty) {
-            if (shadow) return finish(0);
-            lit = lighting(col, normal_from_t(tX, tY, tZ, tMin, d), rwp(), o);
-            return start_shadow(o, false);
-        }
-        float nX = d.x > 0.0f ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
-        float nY = d.y > 0.0f ? ceilf(o.y) + kEps : floorf(o.y) - kEps;
-        float nZ = d.z > 0.0f ? ceilf(o.z) + kEps : floorf(o.z) - kEps;
-        tX = gdiv(nX, o.x, d.x, gd);
-        tY = gdiv(nY, o.y, d.y, gd);
-        tZ = gdiv(nZ, o.z, d.z, gd);
-        tMin = fminf(tX, fminf(tY, tZ));
-        o = add(o, scl(tMin + kEps, d));
+        const bool px = d.x > 0.0f, py = d.y > 0.0f, pz = d.z > 0.0f;
+        const float nX = skip ? (float)(px ? ((vx / 8) + 1) * 8 : (vx / 8) * 8) : (px ? ceilf(o.x) + kEps : floorf(o.x) - kEps);
+        const float nY = skip ? (float)(py ? ((vy / 8) + 1) * 8 : (vy / 8) * 8) : (py ? ceilf(o.y) + kEps : floorf(o.y) - kEps);
+        const float nZ = skip ? (float)(pz ? ((vz / 8) + 1) * 8 : (vz / 8) * 8) : (pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps);
+        const float sX = gdiv(nX, o.x, d.x, gd), sY = gdiv(nY, o.y, d.y, gd), sZ = gdiv(nZ, o.z, d.z, gd);
+        const float sMin = fminf(sX, fminf(sY, sZ));
+        if (!skip) { tX = sX; tY = sY; tZ = sZ; tMin = sMin; }
+        o = add(o, scl(sMin + kEps, d));
         return 0;
     }
 
@@ -337,7 +331,9 @@ constexpr uint32_t kHeadStride = 64;     // one head per 256-B line
 
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(256) void persist_kernel(KScene s, KView v, uint32_t* __restrict__ queue) {
+    __shared__ float inv255_lds[256];
     Machine<STORE, ALGO, COUNT> m(s, v);
+    m.inv255 = load_inv255(inv255_lds);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (v.W + 7u) / 8u;
     const uint32_t ntiles = tiles_x * ((v.local_rows + 7u) / 8u);
@@ -346,58 +342,90 @@ __global__ __launch_bounds__(256) void persist_kernel(KScene s, KView v, uint32_
     uint32_t out_idx = 0;
     uint32_t pool_next = 0, pool_end = 0;      // wave-uniform pixel range
     uint32_t shard = home;
+    // Wave-level scheduling: every iteration runs exactly ONE kind of step for
+    // the lanes in that state (refill, region, DDA, LA, jump), so a wave never
+    // pays for several divergent code blocks in one iteration.  Idle lanes are
+    // refilled in batches of >= kRefillBatch (or when nothing else is left).
+    constexpr uint32_t kRefillBatch = 16;
     for (;;) {
-        for (;;) {   // refill lanes without a pixel
-            const bool need = wave_live && !has;
-            const uint64_t mask = __ballot(need);
-            if (mask == 0) break;
-            if (pool_next == pool_end) {
-                uint32_t got = 0xFFFFFFFFu;
-                if (lane == 0) {
-                    for (uint32_t k = 0; k < kShards; ++k) {
-                        const uint32_t sh = (shard + k) % kShards;
-                        const uint32_t t0 = (uint32_t)(((uint64_t)ntiles * sh) / kShards);
-                        const uint32_t t1 = (uint32_t)(((uint64_t)ntiles * (sh + 1)) / kShards);
-                        uint32_t* head = queue + kHeadStride * sh;
-                        if (__hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= t1 - t0) continue;
-                        const uint32_t t = t0 + atomicAdd(head, 1u);
-                        if (t < t1) { got = t; shard = sh; break; }
-                    }
-                }
-                got = __builtin_amdgcn_readfirstlane(got);
-                shard = __builtin_amdgcn_readfirstlane(shard);
-                if (got == 0xFFFFFFFFu) { wave_live = false; break; }
-                pool_next = got * 64u;
-                pool_end = pool_next + 64u;
+        const uint64_t m_has = __ballot(has);
+        const uint64_t m_need = __ballot(wave_live && !has);
+        if (!m_has && !m_need) break;
+        uint32_t kind;                                    // wave-uniform
+        if (m_need && (!m_has || (uint32_t)__popcll(m_need) >= kRefillBatch)) {
+            kind = 0xFFu;
+        } else {
+            uint32_t best = P_DDA, nbest = (uint32_t)__popcll(__ballot(has && m.phase == P_DDA));
+            const uint32_t nreg = (uint32_t)__popcll(__ballot(has && m.phase == P_REGION));
+            if (nreg > nbest) { best = P_REGION; nbest = nreg; }
+            if (ALGO == ALGO_LONGEST) {
+                const uint32_t nla = (uint32_t)__popcll(__ballot(has && m.phase == P_LA));
+                if (nla > nbest) { best = P_LA; nbest = nla; }
+                const uint32_t nj = (uint32_t)__popcll(__ballot(has && m.phase == P_JUMP));
+                if (nj > nbest) { best = P_JUMP; nbest = nj; }
             }
-            const uint32_t avail = pool_end - pool_next;
-            const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-            if (need && rank < avail) {
-                const uint32_t idx = pool_next + rank;
-                const uint32_t t = idx >> 6, w = idx & 63u;
-                const uint32_t x = (t % tiles_x) * 8u + (w & 7u), l = (t / tiles_x) * 8u + (w >> 3);
-                if (x < v.W && l < v.local_rows) {
-                    out_idx = l * v.W + x;
-                    const uint32_t band = l / v.band_rows;
-                    const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
-                    if (y >= v.row_limit) {
-                        v.out[out_idx] = 0u;
-                    } else if (m.begin_pixel(x, y)) {
-                        v.out[out_idx] = m.aborted ? 0u : m.result;
-                        m.count(4);
-                    } else {
-                        has = true;
-                    }
-                }
-            }
-            const uint32_t n = (uint32_t)__popcll(mask);
-            pool_next += n < avail ? n : avail;
+            kind = best;
         }
-        if (!__any(has)) break;
-        if (has && m.step()) {
-            v.out[out_idx] = m.aborted ? 0u : m.result;
-            m.count(4);
-            has = false;
+        if (kind == 0xFFu) {
+            for (;;) {   // refill lanes without a pixel
+                const bool need = wave_live && !has;
+                const uint64_t mask = __ballot(need);
+                if (mask == 0) break;
+                if (pool_next == pool_end) {
+                    uint32_t got = 0xFFFFFFFFu;
+                    if (lane == 0) {
+                        for (uint32_t k = 0; k < kShards; ++k) {
+                            const uint32_t sh = (shard + k) % kShards;
+                            const uint32_t t0 = (uint32_t)(((uint64_t)ntiles * sh) / kShards);
+                            const uint32_t t1 = (uint32_t)(((uint64_t)ntiles * (sh + 1)) / kShards);
+                            uint32_t* head = queue + kHeadStride * sh;
+                            if (__hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= t1 - t0) continue;
+                            const uint32_t t = t0 + atomicAdd(head, 1u);
+                            if (t < t1) { got = t; shard = sh; break; }
+                        }
+                    }
+                    got = __builtin_amdgcn_readfirstlane(got);
+                    shard = __builtin_amdgcn_readfirstlane(shard);
+                    if (got == 0xFFFFFFFFu) { wave_live = false; break; }
+                    pool_next = got * 64u;
+                    pool_end = pool_next + 64u;
+                }
+                const uint32_t avail = pool_end - pool_next;
+                const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                if (need && rank < avail) {
+                    const uint32_t idx = pool_next + rank;
+                    const uint32_t t = idx >> 6, w = idx & 63u;
+                    const uint32_t x = (t % tiles_x) * 8u + (w & 7u), l = (t / tiles_x) * 8u + (w >> 3);
+                    if (x < v.W && l < v.local_rows) {
+                        out_idx = l * v.W + x;
+                        const uint32_t band = l / v.band_rows;
+                        const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
+                        if (y >= v.row_limit) {
+                            v.out[out_idx] = 0u;
+                        } else if (m.begin_pixel(x, y)) {
+                            v.out[out_idx] = m.aborted ? 0u : m.result;
+                            m.count(4);
+                        } else {
+                            has = true;
+                        }
+                    }
+                }
+                const uint32_t n = (uint32_t)__popcll(mask);
+                pool_next += n < avail ? n : avail;
+            }
+            continue;
+        }
+        if (has && m.phase == kind) {
+            int r;
+            if (kind == P_DDA) r = m.dda_step();
+            else if (ALGO == ALGO_LONGEST && kind == P_LA) r = m.la_step();
+            else if (ALGO == ALGO_LONGEST && kind == P_JUMP) r = m.jump_step();
+            else r = m.region_step();
+            if (r) {
+                v.out[out_idx] = m.aborted ? 0u : m.result;
+                m.count(4);
+                has = false;
+            }
         }
     }
     if (COUNT) {
