@@ -62,6 +62,38 @@ __device__ __forceinline__ uint32_t f2u(float f) {
     return r;
 }
 
+// Correctly rounded n / d with the reciprocal half hoisted out of a walk.
+// hipcc's IEEE f32 division on gfx9 is
+//   ds = v_div_scale(d); r0 = v_rcp_f32(ds); r = fma(fma(-ds, r0, 1), r0, r0);
+//   ns = v_div_scale(n); q = ns * r; q = fma(fma(-ds, q, ns), r, q);
+//   q = v_div_fmas(fma(-ds, q, ns), r, q); v_div_fixup(q, d, n)
+// and for 2^-64 <= |d| <= 2^20 and 2^-90 <= |n| <= 2^20 the two div_scales are
+// the identity (VCC clear, so div_fmas is a plain fma) and div_fixup returns q:
+// div_fast() is that sequence with r computed once per direction, bit-identical
+// to n / d on that domain.  Callers test div_fast_ok() and fall back to `/`.
+struct Rcp { float d, r; bool ok; };
+__device__ __forceinline__ Rcp rcp_setup(float d) {
+    const float r0 = __builtin_amdgcn_rcpf(d);
+    const float r = __builtin_fmaf(__builtin_fmaf(-d, r0, 1.0f), r0, r0);
+    const float a = fabsf(d);
+    return Rcp{d, r, a >= 0x1p-64f && a <= 0x1p+20f};
+}
+__device__ __forceinline__ bool div_fast_ok(float n, const Rcp& c) {
+    const float a = fabsf(n);
+    return c.ok && a >= 0x1p-90f && a <= 0x1p+20f;
+}
+__device__ __forceinline__ float div_fast(float n, const Rcp& c) {
+    float q = n * c.r;
+    q = __builtin_fmaf(__builtin_fmaf(-c.d, q, n), c.r, q);
+    return __builtin_fmaf(__builtin_fmaf(-c.d, q, n), c.r, q);
+}
+// px ? ceilf(o) + EPSILON : floorf(o) - EPSILON, branch-free: with s = +-1,
+// s * (ceilf(s * o) + EPSILON) (floor(o) = -ceil(-o); negation and round-to-
+// nearest commute, so both forms round identically).
+__device__ __forceinline__ float next_plane(float o, float s, float eps) {
+    return s * (ceilf(s * o) + eps);
+}
+
 // CuckooHashTable::hashFunc1 / hashFunc2 (CuckooHashTable.cuh:181-202),
 // int arithmetic with arithmetic right shifts.
 __device__ __forceinline__ uint32_t hash1(uint32_t k, uint32_t offset) {

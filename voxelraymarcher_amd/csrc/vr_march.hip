@@ -53,6 +53,10 @@ struct Walker : Ctx<STORE, COUNT> {
         // before this voxel's search chain, so the two latencies overlap.  On
         // a hit the precomputed step is discarded; the look-ahead directory
         // read is counted only when its iteration runs.
+        // Hoisted reciprocals (div_fast) and +-1 plane signs for the loop.
+        const Rcp rx = rcp_setup(d.x), ry = rcp_setup(d.y), rz = rcp_setup(d.z);
+        const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
+        const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
         uint32_t col = kEmpty;
         while (in_region(o)) {
             if (!tick()) return false;
@@ -63,15 +67,22 @@ struct Walker : Ctx<STORE, COUNT> {
                 col = lookup(reg, blk, vx, vy, vz);
                 if (col != kEmpty) break;
             }
-            const float cX = (float)(px ? ((vx / 8) + 1) * 8 : (vx / 8) * 8);
-            const float cY = (float)(py ? ((vy / 8) + 1) * 8 : (vy / 8) * 8);
-            const float cZ = (float)(pz ? ((vz / 8) + 1) * 8 : (vz / 8) * 8);
-            nX = skip ? cX : (px ? ceilf(o.x) + kEps : floorf(o.x) - kEps);
-            nY = skip ? cY : (py ? ceilf(o.y) + kEps : floorf(o.y) - kEps);
-            nZ = skip ? cZ : (pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps);
-            const float sX = zx ? kInf : (nX - o.x) / d.x;
-            const float sY = zy ? kInf : (nY - o.y) / d.y;
-            const float sZ = zz ? kInf : (nZ - o.z) / d.z;
+            // in_region(o) => vx,vy,vz >= 0, so (v / 8) * 8 == v & ~7
+            nX = skip ? (float)((vx & ~7) + cx8) : next_plane(o.x, gx, kEps);
+            nY = skip ? (float)((vy & ~7) + cy8) : next_plane(o.y, gy, kEps);
+            nZ = skip ? (float)((vz & ~7) + cz8) : next_plane(o.z, gz, kEps);
+            const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
+            float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
+            const bool bx = !zx && !div_fast_ok(ax, rx), by = !zy && !div_fast_ok(ay, ry),
+                       bz = !zz && !div_fast_ok(az, rz);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(bx || by || bz) != 0, 0)) {
+                sX = bx ? ax / d.x : sX;
+                sY = by ? ay / d.y : sY;
+                sZ = bz ? az / d.z : sZ;
+            }
+            sX = zx ? kInf : sX;
+            sY = zy ? kInf : sY;
+            sZ = zz ? kInf : sZ;
             const float sMin = fminf(sX, fminf(sY, sZ));
             if (!skip) { tX = sX; tY = sY; tZ = sZ; tMin = sMin; }
             o = add(o, scl(sMin + kEps, d));
