@@ -77,6 +77,9 @@ def lib() -> ctypes.CDLL:
                                        c_uint32, c_uint32, c_uint32, POINTER(c_uint32), POINTER(c_uint32), c_size_t,
                                        POINTER(c_uint32), POINTER(c_uint64)]
         L.or_render_pixels.restype = c_int
+        L.or_pixel_stats.argtypes = [c_void_p, c_int, POINTER(OrCamera), POINTER(OrLighting), POINTER(c_float),
+                                     c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, POINTER(c_uint64), c_int]
+        L.or_pixel_stats.restype = c_int
         _lib = L
     return _lib
 
@@ -160,6 +163,19 @@ class Scene:
         if rc != 0:
             raise RuntimeError(f"or_render_pixels failed: {rc}")
         return out, b
+
+    def pixel_stats(self, algo: int, cam: OrCamera, lit: OrLighting, width: int, height: int, scale: int,
+                    translation=(0.0, 0.0, 0.0), row_begin: int = 0, row_end: int | None = None, nthreads: int = 0):
+        """-> uint64[rows, width, 2, 7]: per-pixel (primary, shadow) x (region reads, existence
+        checks, cluster skips, lookups, probes, hits, iterations)."""
+        row_end = height if row_end is None else row_end
+        st = np.zeros(((row_end - row_begin), width, 2, 7), dtype=np.uint64)
+        rc = lib().or_pixel_stats(self.h, int(algo), ctypes.byref(cam), ctypes.byref(lit), _f3(translation),
+                                  int(scale), int(width), int(height), int(row_begin), int(row_end),
+                                  st.ctypes.data_as(POINTER(c_uint64)), int(nthreads))
+        if rc != 0:
+            raise RuntimeError(f"or_pixel_stats failed: {rc}")
+        return st
 
     def close(self):
         if self.h:

@@ -942,3 +942,27 @@ int or_render_stats(const or_scene* s, int algo, const or_camera* cam, const or_
         }
     return 0;
 }
+
+/* Per-pixel work statistics of rows [row_begin,row_end): st[(r*width+x)*2*OR_STAT_N + k]
+ * (same counters as or_render_stats), for wave-divergence studies. */
+int or_pixel_stats(const or_scene* s, int algo, const or_camera* cam, const or_lighting* lit,
+                   const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
+                   uint32_t row_begin, uint32_t row_end, uint64_t* st, int nthreads) {
+    if (!s || !cam || !lit || !st || row_end > height || row_begin > row_end) return -1;
+    v3f tr = V3(translation ? translation[0] : 0.0f, translation ? translation[1] : 0.0f,
+                translation ? translation[2] : 0.0f);
+    long rows = (long)(row_end - row_begin);
+    memset(st, 0, sizeof(uint64_t) * 2 * OR_STAT_N * (size_t)rows * width);
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (long r = 0; r < rows; ++r)
+        for (uint32_t x = 0; x < width; ++x) {
+            uint64_t b = 0;
+            (void)render_pixel(s, algo, cam, lit, tr, scale, width, height, x, row_begin + (uint32_t)r, &b,
+                               st + ((size_t)r * width + x) * 2 * OR_STAT_N);
+        }
+    (void)nthreads;
+    return 0;
+}

@@ -101,6 +101,11 @@ int or_render_stats(const or_scene* s, int algo, const or_camera* cam, const or_
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
                     uint32_t row_begin, uint32_t row_end, uint64_t* st);
 
+/* Per-pixel version: st[(r * width + x) * 14 + k] for row r - row_begin. OpenMP. */
+int or_pixel_stats(const or_scene* s, int algo, const or_camera* cam, const or_lighting* lit,
+                   const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
+                   uint32_t row_begin, uint32_t row_end, uint64_t* st, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

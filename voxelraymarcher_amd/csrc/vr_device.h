@@ -70,7 +70,8 @@ __device__ __forceinline__ uint32_t f2u(float f) {
 // and for 2^-64 <= |d| <= 2^20 and 2^-90 <= |n| <= 2^20 the two div_scales are
 // the identity (VCC clear, so div_fmas is a plain fma) and div_fixup returns q:
 // div_fast() is that sequence with r computed once per direction, bit-identical
-// to n / d on that domain.  Callers test div_fast_ok() and fall back to `/`.
+// to n / d on that domain.  Callers test div_fast_ok() (or the bounds it
+// checks: inside a region walk |n| < 73 always) and fall back to `/`.
 struct Rcp { float d, r; bool ok; };
 __device__ __forceinline__ Rcp rcp_setup(float d) {
     const float r0 = __builtin_amdgcn_rcpf(d);
@@ -180,8 +181,18 @@ struct Ctx {
     __device__ __forceinline__ static uint32_t in_cluster(int32_t x, int32_t y, int32_t z) {
         return (((uint32_t)x & 7u) << 6) | (((uint32_t)y & 7u) << 3) | ((uint32_t)z & 7u);
     }
+    // A region's 8192 mask words are stored at word index
+    //   y2 | x0..x5 << 1 | y3..y5 << 7 | z3..z5 << 10   (vcs_word_index)
+    // so a cluster's 16 words are contiguous (one 128-B record, in-cluster
+    // word w = (x&7)<<1 | y2 as before) and the index of an in-region voxel
+    // is a few bit operations.
     __device__ __forceinline__ const uint2* masks(uint32_t reg, int32_t cid) const {
-        return s.vcs_mask + ((size_t)(reg * 512u + (uint32_t)cid) << 4);
+        const uint32_t c = (uint32_t)cid;
+        const uint32_t slot = (c >> 6) | (((c >> 3) & 7u) << 3) | ((c & 7u) << 6);
+        return s.vcs_mask + (size_t)reg * 8192u + (slot << 4);
+    }
+    __device__ __forceinline__ static uint32_t word_index(uint32_t x, uint32_t y, uint32_t z) {   // x,y,z < 64
+        return ((y >> 2) & 1u) | (x << 1) | ((y & 0x38u) << 4) | ((z & 0x38u) << 7);
     }
 
     // doesVoxelSpaceExist (StorageStructure.cuh:29-32,49-52) ->
@@ -191,6 +202,11 @@ struct Ctx {
     __device__ __forceinline__ Blk exists(uint32_t reg, int32_t x, int32_t y, int32_t z) {
         if (STORE == STORE_HASH) return Blk{0u, 0u};
         count(4);
+        return mask_word(reg, x, y, z);
+    }
+    // The read behind exists() without its byte count (for walks that request
+    // it ahead and count it when the iteration that needs it runs).
+    __device__ __forceinline__ Blk mask_word(uint32_t reg, int32_t x, int32_t y, int32_t z) const {
         const int32_t cid = cluster_id(x, y, z);
         if (cid < 0) return Blk{0u, kNone};
         return masks(reg, cid)[in_cluster(x, y, z) >> 5];
@@ -309,6 +325,12 @@ struct Ctx {
 
     __device__ __forceinline__ static bool in_region(f3 o) {               // Renderer.cuh:93-98
         return o.x >= 0.0f && o.x < 64.0f && o.y >= 0.0f && o.y < 64.0f && o.z >= 0.0f && o.z < 64.0f;
+    }
+    // The same predicate on the float encodings: after x + 0.0f (which turns
+    // -0 into +0 and keeps NaN), x in [0, 64) <=> bits(x) < bits(64.0f).
+    __device__ __forceinline__ static bool in_region_bits(f3 o) {
+        const uint32_t a = __float_as_uint(o.x + 0.0f), b = __float_as_uint(o.y + 0.0f), c = __float_as_uint(o.z + 0.0f);
+        return max(max(a, b), c) < 0x42800000u;
     }
     __device__ __forceinline__ static bool grid_in_region(int32_t a, int32_t b, int32_t c) {   // :436-439
         return (uint32_t)a < 64u && (uint32_t)b < 64u && (uint32_t)c < 64u;

@@ -284,7 +284,9 @@ int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* 
             }
             for (uint32_t c = 0; c < 512; ++c) {
                 if (!cnt[c]) continue;
-                uint2* w = &mask[((size_t)r * 512 + c) * 16];
+                // slot order z3..5 | y3..5 | x3..5 (vr_device.h word_index)
+                const uint32_t slot = (c >> 6) | (((c >> 3) & 7u) << 3) | ((c & 7u) << 6);
+                uint2* w = &mask[((size_t)r * 512 + slot) * 16];
                 uint32_t run = start[c];
                 for (uint32_t j = 0; j < 16; ++j) {
                     w[j] = uint2{bits[c][j], run};

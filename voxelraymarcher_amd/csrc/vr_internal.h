@@ -14,13 +14,16 @@ constexpr uint32_t kIterBudget = 65536u;     // per-pixel hang guard
 
 // Device view of one immutable scene.  All offsets are 32-bit word indices.
 //  region_slot[D^3]          : region index r, or kNone (null StorageStructure*)
-//  VCS   : vcs_mask[((r*512+cid)*16 + w]  (one 128-B record per cluster slot of an
+//  VCS   : vcs_mask[r*8192 + slot*16 + w]  (one 128-B record per cluster of an
 //                              occupied region; VoxelClusterStore::deviceBlockMemAddress
 //                              + the cluster's sorted keys, VoxelClusterStore.cuh:37-85)
 //                              {bits, index}: bit b set <=> the voxel with in-cluster index
 //                              q = 32w+b ((x&7)<<6|(y&7)<<3|z&7, the keys' order) is stored;
 //                              index = vcs_vals position of the word's first stored voxel.
-//                              Absent cluster: {0, kNone} in all 16 words.
+//                              Absent cluster: {0, kNone} in all 16 words.  slot =
+//                              z-cluster<<6 | y-cluster<<3 | x-cluster (a permutation of the
+//                              reference's cluster id x<<6|y<<3|z, so that the word of an
+//                              in-region voxel is y2 | x<<1 | (y>>3)<<7 | (z>>3)<<10).
 //          vcs_vals[]        : colours, cluster by cluster in key order.
 //  Cuckoo: ht_meta[r]        : {base, M, prime, offset}
 //          ht_slots[base+i]  : table 1 slot i {key, value};

@@ -48,44 +48,84 @@ struct Walker : Ctx<STORE, COUNT> {
         float tZ = zz ? kInf : (nZ - o.z) / d.z;
         float tMin = fminf(tX, fminf(tY, tZ));
         o = add(o, scl(tMin + kEps, d));
-        // Software-pipelined: the step for this voxel is computed before its
-        // lookup, and the directory entry of the next voxel is requested
-        // before this voxel's search chain, so the two latencies overlap.  On
-        // a hit the precomputed step is discarded; the look-ahead directory
-        // read is counted only when its iteration runs.
         // Hoisted reciprocals (div_fast) and +-1 plane signs for the loop.
         const Rcp rx = rcp_setup(d.x), ry = rcp_setup(d.y), rz = rcp_setup(d.z);
         const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
         const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
+        const bool walk_ok = (zx || rx.ok) && (zy || ry.ok) && (zz || rz.ok);
         uint32_t col = kEmpty;
-        while (in_region(o)) {
-            if (!tick()) return false;
-            const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-            const Blk blk = exists(reg, vx, vy, vz);
-            const bool skip = absent(blk);
-            if (!skip) {
-                col = lookup(reg, blk, vx, vy, vz);
-                if (col != kEmpty) break;
+        if constexpr (STORE == STORE_VCS) {
+            // Inside the region every voxel coordinate is in [0, 64): the mask
+            // word index is a few bit operations and the lookup needs no
+            // range check (Ctx::lookup's general form handles the rest).
+            const uint2* mreg = s.vcs_mask + (size_t)reg * 8192u;
+            while (this->in_region_bits(o)) {
+                if (!tick()) return false;
+                const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
+                this->count(4);
+                const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
+                Blk blk = mreg[wi];
+                // both candidate planes, computed while the mask word is in
+                // flight and materialised (with the whole 8-B word: one load)
+                // before the branch below
+                float vX = next_plane(o.x, gx, kEps), vY = next_plane(o.y, gy, kEps), vZ = next_plane(o.z, gz, kEps);
+                float cX = (float)((vx & ~7) + cx8), cY = (float)((vy & ~7) + cy8), cZ = (float)((vz & ~7) + cz8);
+                asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
+                const bool skip = absent(blk);
+                if (!skip) {
+                    const uint32_t bit = (((uint32_t)vy & 3u) << 3) | ((uint32_t)vz & 7u);
+                    const bool found = (blk.x >> bit) & 1u;
+                    const uint32_t vi = blk.y + __popc(blk.x & ((1u << bit) - 1u));
+                    if (COUNT) this->count_bsearch(mreg + (wi & ~15u), vi, found);
+                    if (found) { col = s.vcs_vals[vi]; break; }
+                }
+                nX = skip ? cX : vX;
+                nY = skip ? cY : vY;
+                nZ = skip ? cZ : vZ;
+                const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
+                float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
+                const bool bad = !walk_ok || !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= 0x1p-90f);
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                    sX = bad ? ax / d.x : sX;
+                    sY = bad ? ay / d.y : sY;
+                    sZ = bad ? az / d.z : sZ;
+                }
+                sX = zx ? kInf : sX;
+                sY = zy ? kInf : sY;
+                sZ = zz ? kInf : sZ;
+                const float sMin = fminf(sX, fminf(sY, sZ));
+                if (!skip) { tX = sX; tY = sY; tZ = sZ; tMin = sMin; }
+                o = add(o, scl(sMin + kEps, d));
             }
-            // in_region(o) => vx,vy,vz >= 0, so (v / 8) * 8 == v & ~7
-            nX = skip ? (float)((vx & ~7) + cx8) : next_plane(o.x, gx, kEps);
-            nY = skip ? (float)((vy & ~7) + cy8) : next_plane(o.y, gy, kEps);
-            nZ = skip ? (float)((vz & ~7) + cz8) : next_plane(o.z, gz, kEps);
-            const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
-            float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
-            const bool bx = !zx && !div_fast_ok(ax, rx), by = !zy && !div_fast_ok(ay, ry),
-                       bz = !zz && !div_fast_ok(az, rz);
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(bx || by || bz) != 0, 0)) {
-                sX = bx ? ax / d.x : sX;
-                sY = by ? ay / d.y : sY;
-                sZ = bz ? az / d.z : sZ;
+        } else {
+            while (in_region(o)) {
+                if (!tick()) return false;
+                const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
+                const Blk blk = exists(reg, vx, vy, vz);
+                const bool skip = absent(blk);
+                if (!skip) {
+                    col = lookup(reg, blk, vx, vy, vz);
+                    if (col != kEmpty) break;
+                }
+                // in_region(o) => vx,vy,vz >= 0, so (v / 8) * 8 == v & ~7
+                nX = skip ? (float)((vx & ~7) + cx8) : next_plane(o.x, gx, kEps);
+                nY = skip ? (float)((vy & ~7) + cy8) : next_plane(o.y, gy, kEps);
+                nZ = skip ? (float)((vz & ~7) + cz8) : next_plane(o.z, gz, kEps);
+                const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
+                float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
+                const bool bad = !walk_ok || !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= 0x1p-90f);
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                    sX = bad ? ax / d.x : sX;
+                    sY = bad ? ay / d.y : sY;
+                    sZ = bad ? az / d.z : sZ;
+                }
+                sX = zx ? kInf : sX;
+                sY = zy ? kInf : sY;
+                sZ = zz ? kInf : sZ;
+                const float sMin = fminf(sX, fminf(sY, sZ));
+                if (!skip) { tX = sX; tY = sY; tZ = sZ; tMin = sMin; }
+                o = add(o, scl(sMin + kEps, d));
             }
-            sX = zx ? kInf : sX;
-            sY = zy ? kInf : sY;
-            sZ = zz ? kInf : sZ;
-            const float sMin = fminf(sX, fminf(sY, sZ));
-            if (!skip) { tX = sX; tY = sY; tZ = sZ; tMin = sMin; }
-            o = add(o, scl(sMin + kEps, d));
         }
         if (col == kEmpty) return false;
         if (!SHADOW) {
