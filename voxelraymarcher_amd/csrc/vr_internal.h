@@ -52,6 +52,7 @@ struct KView {
     uint32_t row0, band_rows, rank, nranks, local_rows, row_limit;
     uint32_t* out;
     unsigned long long* bytes;
+    uint32_t experiment;      // VR_EXPERIMENT (tuning A/B only; 0 in production)
 };
 
 // Launch one render (defined in vr_march.hip).

@@ -59,26 +59,31 @@ struct Walker : Ctx<STORE, COUNT> {
             // word index is a few bit operations and the lookup needs no
             // range check (Ctx::lookup's general form handles the rest).
             const uint2* mreg = s.vcs_mask + (size_t)reg * 8192u;
-            while (this->in_region_bits(o)) {
-                if (!tick()) return false;
+            // Straight-line body with one exit: the hit test, the region test of
+            // the stepped position and the iteration budget are folded into a
+            // single condition; the step of the hit iteration is computed and
+            // discarded (the reference breaks before it).  tick() semantics are
+            // kept: iteration k of the pixel runs iff k <= kIterBudget.
+            if (!this->in_region_bits(o)) return false;
+            if (aborted || this->iters >= kIterBudget) { aborted = true; return false; }
+            bool found = false, inside = true;
+            uint32_t vi = 0;
+            for (;;) {
+                ++this->iters;
                 const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
                 this->count(4);
                 const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
                 Blk blk = mreg[wi];
                 // both candidate planes, computed while the mask word is in
                 // flight and materialised (with the whole 8-B word: one load)
-                // before the branch below
                 float vX = next_plane(o.x, gx, kEps), vY = next_plane(o.y, gy, kEps), vZ = next_plane(o.z, gz, kEps);
                 float cX = (float)((vx & ~7) + cx8), cY = (float)((vy & ~7) + cy8), cZ = (float)((vz & ~7) + cz8);
                 asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
                 const bool skip = absent(blk);
-                if (!skip) {
-                    const uint32_t bit = (((uint32_t)vy & 3u) << 3) | ((uint32_t)vz & 7u);
-                    const bool found = (blk.x >> bit) & 1u;
-                    const uint32_t vi = blk.y + __popc(blk.x & ((1u << bit) - 1u));
-                    if (COUNT) this->count_bsearch(mreg + (wi & ~15u), vi, found);
-                    if (found) { col = s.vcs_vals[vi]; break; }
-                }
+                const uint32_t bit = (((uint32_t)vy & 3u) << 3) | ((uint32_t)vz & 7u);
+                found = (!skip) & (((blk.x >> bit) & 1u) != 0u);
+                vi = blk.y + __popc(blk.x & ((1u << bit) - 1u));
+                if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
                 nX = skip ? cX : vX;
                 nY = skip ? cY : vY;
                 nZ = skip ? cZ : vZ;
@@ -94,9 +99,20 @@ struct Walker : Ctx<STORE, COUNT> {
                 sY = zy ? kInf : sY;
                 sZ = zz ? kInf : sZ;
                 const float sMin = fminf(sX, fminf(sY, sZ));
-                if (!skip) { tX = sX; tY = sY; tZ = sZ; tMin = sMin; }
-                o = add(o, scl(sMin + kEps, d));
+                const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
+                tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
+                const f3 on = add(o, scl(sMin + kEps, d));
+                inside = this->in_region_bits(on);
+                o.x = found ? o.x : on.x;   // per component: a struct-valued ?: goes through scratch
+                o.y = found ? o.y : on.y;
+                o.z = found ? o.z : on.z;
+                if (found || !inside || this->iters >= kIterBudget) break;
             }
+            if (!found) {
+                if (inside) aborted = true;     // the next iteration's tick() would have failed
+                return false;
+            }
+            col = s.vcs_vals[vi];
         } else {
             while (in_region(o)) {
                 if (!tick()) return false;
@@ -357,8 +373,9 @@ __global__ __launch_bounds__(256, ALGO == ALGO_ORIGINAL ? 7 : 3) void march_kern
     __shared__ float inv255_lds[256];
     const float* inv255 = load_inv255(inv255_lds);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t x = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
-    const uint32_t l = (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
+    const uint32_t bx = blockIdx.x, by = blockIdx.y;
+    const uint32_t x = (bx * 2u + (wave & 1u)) * 8u + (lane & 7u);
+    const uint32_t l = (by * 2u + (wave >> 1)) * 8u + (lane >> 3);
     uint32_t bytes = 0;
     if (x < v.W && l < v.local_rows) {
         const uint32_t band = l / v.band_rows;
