@@ -346,19 +346,15 @@ struct Ctx {
     // Null-region skip body (Renderer.cuh:386-409; guarded form :187-210).
     template <bool GUARDED>
     __device__ __forceinline__ bool skip_null(i3& cr, f3& o, f3 d, uint32_t& reg) {
+        return skip_null_rt(cr, o, d, reg, GUARDED);
+    }
+    __device__ __forceinline__ bool skip_null_rt(i3& cr, f3& o, f3 d, uint32_t& reg, const bool GUARDED) {
         float nx = d.x > 0.0f ? 64.0f + kEps : 0.0f - kEps;
         float ny = d.y > 0.0f ? 64.0f + kEps : 0.0f - kEps;
         float nz = d.z > 0.0f ? 64.0f + kEps : 0.0f - kEps;
-        float tX, tY, tZ;
-        if (GUARDED) {
-            tX = d.x != 0.0f ? (nx - o.x) / d.x : kInf;
-            tY = d.y != 0.0f ? (ny - o.y) / d.y : kInf;
-            tZ = d.z != 0.0f ? (nz - o.z) / d.z : kInf;
-        } else {
-            tX = (nx - o.x) / d.x;
-            tY = (ny - o.y) / d.y;
-            tZ = (nz - o.z) / d.z;
-        }
+        const float tX = (GUARDED && d.x == 0.0f) ? kInf : (nx - o.x) / d.x;
+        const float tY = (GUARDED && d.y == 0.0f) ? kInf : (ny - o.y) / d.y;
+        const float tZ = (GUARDED && d.z == 0.0f) ? kInf : (nz - o.z) / d.z;
         float tMin = fminf(tX, fminf(tY, tZ));
         o = add(o, scl(tMin, d));
         advance_region(cr, o);

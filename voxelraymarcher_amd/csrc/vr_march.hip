@@ -38,6 +38,11 @@ struct Walker : Ctx<STORE, COUNT> {
     // caller after the walk (Hit carries colour, normal and position).
     template <bool SHADOW>
     __device__ __forceinline__ bool grid_original(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h) {
+        return grid_original_rt(o, d, reg, cr, h, SHADOW);
+    }
+    // The same with the shadow flag a per-lane value (fused primary + shadow
+    // walk); the template form above constant-folds it.
+    __device__ __forceinline__ bool grid_original_rt(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h, const bool SHADOW) {
         const bool px = d.x > 0.0f, py = d.y > 0.0f, pz = d.z > 0.0f;
         const bool zx = SHADOW && d.x == 0.0f, zy = SHADOW && d.y == 0.0f, zz = SHADOW && d.z == 0.0f;
         float nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
@@ -52,7 +57,9 @@ struct Walker : Ctx<STORE, COUNT> {
         const Rcp rx = rcp_setup(d.x), ry = rcp_setup(d.y), rz = rcp_setup(d.z);
         const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
         const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
-        const bool walk_ok = (zx || rx.ok) && (zy || ry.ok) && (zz || rz.ok);
+        // A guarded zero direction component (shadow ray) keeps the lane on the
+        // slow branch, which applies the guard: the fast path needs no selects.
+        const bool walk_ok = rx.ok && ry.ok && rz.ok && !zx && !zy && !zz;
         uint32_t col = kEmpty;
         if constexpr (STORE == STORE_VCS) {
             // Inside the region every voxel coordinate is in [0, 64): the mask
@@ -68,12 +75,13 @@ struct Walker : Ctx<STORE, COUNT> {
             if (aborted || this->iters >= kIterBudget) { aborted = true; return false; }
             bool found = false, inside = true;
             uint32_t vi = 0;
+            Blk blk;
             for (;;) {
                 ++this->iters;
                 const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
                 this->count(4);
                 const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
-                Blk blk = mreg[wi];
+                blk = mreg[wi];
                 // both candidate planes, computed while the mask word is in
                 // flight and materialised (with the whole 8-B word: one load)
                 float vX = next_plane(o.x, gx, kEps), vY = next_plane(o.y, gy, kEps), vZ = next_plane(o.z, gz, kEps);
@@ -91,13 +99,10 @@ struct Walker : Ctx<STORE, COUNT> {
                 float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
                 const bool bad = !walk_ok || !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= 0x1p-90f);
                 if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                    sX = bad ? ax / d.x : sX;
-                    sY = bad ? ay / d.y : sY;
-                    sZ = bad ? az / d.z : sZ;
+                    sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                    sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                    sZ = bad ? (zz ? kInf : az / d.z) : sZ;
                 }
-                sX = zx ? kInf : sX;
-                sY = zy ? kInf : sY;
-                sZ = zz ? kInf : sZ;
                 const float sMin = fminf(sX, fminf(sY, sZ));
                 const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
                 tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
@@ -131,13 +136,10 @@ struct Walker : Ctx<STORE, COUNT> {
                 float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
                 const bool bad = !walk_ok || !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= 0x1p-90f);
                 if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                    sX = bad ? ax / d.x : sX;
-                    sY = bad ? ay / d.y : sY;
-                    sZ = bad ? az / d.z : sZ;
+                    sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                    sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                    sZ = bad ? (zz ? kInf : az / d.z) : sZ;
                 }
-                sX = zx ? kInf : sX;
-                sY = zy ? kInf : sY;
-                sZ = zz ? kInf : sZ;
                 const float sMin = fminf(sX, fminf(sY, sZ));
                 if (!skip) { tX = sX; tY = sY; tZ = sZ; tMin = sMin; }
                 o = add(o, scl(sMin + kEps, d));
