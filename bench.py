@@ -5,11 +5,14 @@ roofline of the dominant kernel and the CPU oracle baseline.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
 
-A step = one full frame: every rank renders its interleaved row bands
-(band b -> rank b % N; one rank = the whole frame), then (N > 1) the bands are
-gathered to rank 0 over RCCL and reassembled.  The frame is fixed while N
-grows ("scaling": "strong").  Inputs (scene, camera) are resident in HBM
-before timing starts.  Rank 0 prints ONE JSON line.
+A step = one full frame.  N = 1: the C2 frame exactly.  N > 1 (one rank per
+GPU, torch.distributed.run, RCCL): weak scaling over image tiles -- the same
+view at N x the pixels (each side x sqrt(N), ~1920x1080 per GPU), rows split
+into interleaved 8-row bands (band b -> rank b % N), and every frame gathered
+to rank 0 over RCCL and assembled there; the gather of frame k runs beside the
+render of frame k+1 (tiles.BandGather, two band buffers).  Inputs (scene,
+camera) are resident in HBM before timing starts; the timed region ends after
+the last frame's gather and assembly.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -27,7 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import voxelraymarcher_amd as vr  # noqa: E402
-from voxelraymarcher_amd.tiles import assemble_bands  # noqa: E402
+from voxelraymarcher_amd.tiles import BandGather, weak_scaled_resolution  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 BAND_ROWS = 8              # one wave tile high
@@ -84,41 +87,34 @@ def main():
     cfg = vr.CONFIGS[args.config]
     xyz, rgb = cfg.voxels()
     scene = vr.create_scene(xyz, rgb, cfg.store, device=local)
-    W, H = cfg.width, cfg.height
+    W, H = weak_scaled_resolution(cfg.width, cfg.height, world)
     cam = vr.Camera.reference(W, H)
     lit = vr.setup_constant_values()
     info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
-    words = vr.band_buffer_words(W, H, BAND_ROWS, world)
-    buf = torch.empty(words, dtype=torch.int32, device=dev)
-    gathered = [torch.empty_like(buf) for _ in range(world)] if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream()
+    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=2)
 
-    def render():
+    def render(buf):
         vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, rank, world, buf, stream)
 
-    def step():
-        render()
-        if world > 1:
-            dist.gather(buf, gathered, dst=0)
-            if rank == 0:
-                assemble_bands(torch.stack(gathered), W, H, BAND_ROWS)
-
-    # algorithmic bytes of one launch (instrumented kernel, untimed)
+    # algorithmic bytes of the frame (instrumented kernel, untimed)
     ctr = torch.zeros(1, dtype=torch.int64, device=dev)
     full = torch.empty(W * H, dtype=torch.int32, device=dev)
     vr.render_count(scene, cfg.algorithm, cam, lit, info, W, H, full, ctr)
     torch.cuda.synchronize()
     frame_bytes = int(ctr.item())
+    del full
 
     for _ in range(args.warmup):
-        step()
+        pipe.step(render)
+    pipe.drain()
     torch.cuda.synchronize()
 
-    # kernel-only timing on the launch stream (HIP events), untimed region for the step clock
+    # kernel-only timing of this rank's launch on the launch stream (HIP events)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     for a, b in ev:
         a.record(stream)
-        render()
+        render(pipe.bufs[0])
         b.record(stream)
     torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -128,7 +124,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        pipe.step(render)
+    pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -161,14 +158,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (counter-hash voxel grid, SURVEY.md 8(d))",
-            "config": {"workload": f"{cfg.name}: {cfg.notes}", "grid": cfg.grid, "width": W, "height": H,
+            "config": {"workload": f"{cfg.name}: {cfg.notes}" + (
+                           "" if world == 1 else f"; the same view at {W}x{H} (x{world} pixels, weak scaling)"),
+                       "grid": cfg.grid, "width": W, "height": H,
                        "store": cfg.store.name, "algorithm": cfg.algorithm.name, "scale": cfg.scale,
                        "voxels": int(len(rgb)), "parallelism": f"row-band tiles x{world}" +
-                       (" + RCCL gather" if world > 1 else "")},
+                       (" + RCCL gather to rank 0 (overlapped with the next frame)" if world > 1 else "")},
             "kernel_ms": round(kern_ms, 4),
             "kernel_mrays_per_s": round(W * H / world / (kern_ms * 1e-3) / 1e6, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -5,6 +5,8 @@ gather of the framebuffer to rank 0.
 """
 from __future__ import annotations
 
+import math
+
 import torch
 
 from .renderer import band_buffer_words
@@ -33,3 +35,70 @@ def owned_rows(height: int, band_rows: int, rank: int, nranks: int) -> list[int]
     for b in range(rank, nb, nranks):
         rows.extend(range(b * band_rows, min(height, (b + 1) * band_rows)))
     return rows
+
+
+def weak_scaled_resolution(width: int, height: int, nranks: int) -> tuple[int, int]:
+    """The same view at about nranks x the pixels (both sides x sqrt(nranks), so the
+    aspect ratio -- and with it Camera::Camera's view -- stays put and every rank
+    renders about width x height pixels).  nranks = 1 gives (width, height)."""
+    f = math.sqrt(nranks)
+    return int(round(width * f)), int(round(height * f))
+
+
+class BandGather:
+    """Row-band image tiling across ranks with the gather to rank 0 overlapped.
+
+    step(render) renders this rank's bands of the next frame into one of `depth`
+    band buffers and starts an asynchronous gather of it to rank 0 (RCCL on
+    GPUs, gloo on CPU); the buffer is reused `depth` frames later, after that
+    gather has completed, and rank 0 then assembles the frame into `frame`
+    (one permuting copy).  So frame k's gather runs beside frame k+1's render.
+    drain() completes every outstanding frame.  With one rank the band buffer
+    already is the frame (bands in row order) and nothing is exchanged.
+    """
+
+    def __init__(self, width: int, height: int, band_rows: int, rank: int, nranks: int,
+                 device, depth: int = 2, on_frame=None):
+        self.W, self.H, self.B = width, height, band_rows
+        self.rank, self.R, self.depth = rank, nranks, depth
+        words = band_buffer_words(width, height, band_rows, nranks)
+        self.per = bands_per_rank(height, band_rows, nranks)
+        self.bufs = [torch.empty(words, dtype=torch.int32, device=device) for _ in range(depth)]
+        self.recv = ([torch.empty((nranks, words), dtype=torch.int32, device=device) for _ in range(depth)]
+                     if (rank == 0 and nranks > 1) else None)
+        self.frame = (torch.empty((self.per * nranks * band_rows, width), dtype=torch.int32, device=device)
+                      if rank == 0 else None)
+        self.work = [None] * depth
+        self.pending = []            # slots in submission order
+        self.on_frame = on_frame     # rank 0: callback(frame[:H]) after each assembled frame
+        self.k = 0
+
+    def _finish(self, slot: int) -> None:
+        if self.R == 1:
+            if self.on_frame is not None:
+                self.on_frame(self.bufs[slot].view(-1, self.W)[:self.H])
+        else:
+            self.work[slot].wait()
+            self.work[slot] = None
+            if self.rank == 0:
+                src = self.recv[slot].view(self.R, self.per, self.B, self.W).permute(1, 0, 2, 3)
+                self.frame.view(self.per, self.R, self.B, self.W).copy_(src)
+                if self.on_frame is not None:
+                    self.on_frame(self.frame[:self.H])
+        self.pending.remove(slot)
+
+    def step(self, render) -> None:
+        slot = self.k % self.depth
+        if slot in self.pending:
+            self._finish(slot)
+        render(self.bufs[slot])
+        if self.R > 1:
+            import torch.distributed as dist
+            dst = list(self.recv[slot].unbind(0)) if self.rank == 0 else None
+            self.work[slot] = dist.gather(self.bufs[slot], dst, dst=0, async_op=True)
+        self.pending.append(slot)
+        self.k += 1
+
+    def drain(self) -> None:
+        while self.pending:
+            self._finish(self.pending[0])
