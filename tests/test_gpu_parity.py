@@ -91,6 +91,21 @@ def test_c5_sparse_rows():
                     row_begin=1000, row_end=1016, oracle_scene=o, gpu_scene=g)
 
 
+def test_c5_crawl_rows():
+    """C5 rows 696-712: thousands of rays that creep through empty clusters by
+    RN(EPSILON * d) per iteration (o pinned on a cluster plane), most of
+    them until the 65 536-iteration budget -- including a ties-to-even crawl at
+    (792, 709).  The tile pass defers them and the crawl pass fast-forwards them;
+    pixels and algorithmic bytes must still equal the oracle's plain walk."""
+    cfg = vr.CONFIGS["C5"]
+    xyz, rgb = cfg.voxels()
+    g = vr.create_scene(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE)
+    o = oracle.Scene(xyz, rgb, 0)
+    for algo in ALGOS:
+        check_frame(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE, algo, cfg.width, cfg.height, cfg.scale,
+                    row_begin=696, row_end=712, oracle_scene=o, gpu_scene=g)
+
+
 def test_count_variant_pixels_identical(c2):
     cfg = vr.CONFIGS["C2"]
     scene = vr.create_scene(*c2, vr.StorageType.VOXEL_CLUSTER_STORE)

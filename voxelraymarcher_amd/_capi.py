@@ -18,7 +18,8 @@ from ctypes import (POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_size
 import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libvr.so")
+# VR_LIBRARY selects another in-tree build of the same ABI (A/B tuning runs).
+LIB_PATH = os.environ.get("VR_LIBRARY") or os.path.join(HERE, "libvr.so")
 
 VR_OK = 0
 ERRORS = {-1: "VR_E_INVALID", -2: "VR_E_HIP", -3: "VR_E_NOMEM", -4: "VR_E_IO", -5: "VR_E_BUILD", -6: "VR_E_PARSE"}

@@ -398,6 +398,36 @@ int queue_slot(int dev, uint32_t** out) {
     return VR_OK;
 }
 
+// Per-device ring of crawl-deferral slots (vr::kDeferWords uint32 each, zeroed
+// once; the crawl pass resets its slot at its end), one per launch in flight.
+constexpr uint32_t kDeferSlots = 64;
+struct DeferRing {
+    std::mutex mu;
+    uint32_t* base[64] = {nullptr};
+    std::atomic<uint32_t> next{0};
+};
+DeferRing g_defer;
+
+int defer_slot(int dev, uint32_t** out) {
+    if (dev < 0 || dev >= 64) return fail(VR_E_INVALID, "device index too large");
+    if (!g_defer.base[dev]) {
+        std::lock_guard<std::mutex> lk(g_defer.mu);
+        if (!g_defer.base[dev]) {
+            void* p = nullptr;
+            const size_t bytes = (size_t)kDeferSlots * vr::kDeferWords * sizeof(uint32_t);
+            hipError_t e = hipMalloc(&p, bytes);
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(defer ring)");
+            e = hipMemset(p, 0, bytes);
+            if (e != hipSuccess) return hip_fail(e, "hipMemset(defer ring)");
+            e = hipDeviceSynchronize();
+            if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+            g_defer.base[dev] = (uint32_t*)p;
+        }
+    }
+    *out = g_defer.base[dev] + (size_t)vr::kDeferWords * (g_defer.next.fetch_add(1) % kDeferSlots);
+    return VR_OK;
+}
+
 int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void* stream) {
     if (algo != VR_ALGO_ORIGINAL && algo != VR_ALGO_LONGESTAXIS) return fail(VR_E_INVALID, "unknown algorithm");
     if (v.local_rows == 0 || v.W == 0) return VR_OK;
@@ -406,6 +436,11 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void*
     hipError_t e;
     if (kernel == VR_KERNEL_AUTO) kernel = VR_KERNEL_TILE;   // measured fastest for every pair
     if (kernel == VR_KERNEL_TILE) {
+        if (s->store == VR_STORE_VCS) {           // cluster-skip crawls: deferred to a second pass
+            int rc = defer_slot(s->device, &v.defer);
+            if (rc) return rc;
+            v.defer_cap = vr::kDeferCap;
+        }
         e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, (hipStream_t)stream);
     } else {
         uint32_t* q = nullptr;

@@ -52,8 +52,15 @@ struct KView {
     uint32_t row0, band_rows, rank, nranks, local_rows, row_limit;
     uint32_t* out;
     unsigned long long* bytes;
+    uint32_t* defer;          // crawl deferral slot: [count, done, entries (l << 16 | x)...]
+    uint32_t defer_cap;
     uint32_t experiment;      // VR_EXPERIMENT (tuning A/B only; 0 in production)
 };
+
+// Rays that start a cluster-skip crawl (see vr_march.hip crawl_steps) in the
+// tile pass are deferred to a second pass over a per-launch list.
+constexpr uint32_t kDeferCap = 65536;
+constexpr uint32_t kDeferWords = 2 + kDeferCap;
 
 // Launch one render (defined in vr_march.hip).
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,

@@ -20,7 +20,77 @@
 namespace vr {
 namespace {
 
-template <int STORE, bool COUNT>
+// Exact fast-forward of a cluster-skip crawl (rayMarchVoxelGrid's skip branch,
+// Renderer.cuh:290-306, with tMin = +-0).  An iteration started in an absent
+// cluster, found t = 0 on an axis whose skip plane is the position itself and
+// moved to `on` = o + RN(EPSILON * d) componentwise.  While the positions stay
+// in that cluster and, per axis, in one binade, every further iteration is the
+// same skip: t = 0 on the same (unmoved) axis -- every other t is >= 0 -- and
+// o_i <- RN(o_i + c_i), c_i = RN(EPSILON * d_i), i.e. o_i += delta_i, a fixed
+// multiple of the binade's ulp (for a tie c_i / ulp = k + 1/2 only from an even
+// mantissa, where every step lands on an even mantissa again).  Returns the number
+// m of such iterations (0 = none, at most `room`) and the per-axis deltas; the
+// caller credits m loop iterations and m existence reads.
+struct Crawl { uint32_t m; float dx, dy, dz; };
+// One axis: returns false to decline; else sets its delta, ORs in whether it is
+// pinned on its skip plane, and lowers m to a number of iterations its binade and
+// the cluster certainly allow (the float quotients are shrunk by 2^-20, so m may
+// come out a little low -- the walk then simply runs those iterations -- never high).
+__device__ __forceinline__ float crawl_floor(float num, float den) {
+    return floorf(num * __builtin_amdgcn_rcpf(den) * (1.0f - 0x1p-20f));
+}
+__device__ __forceinline__ bool crawl_axis(float x, float dir, int32_t v, bool pos, float& delta, bool& pinned,
+                                           float& m) {
+    const float c = kEps * dir, nx = x + c;
+    const float cl = (float)(v & ~7);                                           // cluster [cl, cl + 8)
+    if (nx == x) {
+        delta = 0.0f;
+        pinned |= !pos && cl == x;
+        return true;
+    }
+    if (!(x >= 0x1p-100f)) return false;     // zero / tiny coordinate: no binade arithmetic
+    const uint32_t bits = __float_as_uint(x), be = bits >> 23;                  // x > 0: biased exponent
+    const float lo = __uint_as_float(be << 23), hi = __uint_as_float((be + 1u) << 23);
+    if (!(nx >= lo && nx < hi)) return false;
+    const float x1 = __uint_as_float(bits + 1u), x2 = __uint_as_float(bits + 2u);
+    delta = nx - x;                           // exact (same binade)
+    if (!(x2 < hi)) return false;
+    if ((x1 + c) - x1 != delta) {
+        // c / ulp = k + 1/2: ties-to-even makes every result's mantissa even, so
+        // from an even mantissa the step is constant (checked on the next even one).
+        if ((bits & 1u) || (x2 + c) - x2 != delta) return false;
+    }
+    // positions x + t*delta: t = 0..m inside [lo, hi), t = 0..m-1 inside [cl, cl + 8)
+    m = delta > 0.0f ? fminf(m, fminf(crawl_floor(hi - x, delta), crawl_floor(cl + 8.0f - x, delta)))
+                     : fminf(m, fminf(crawl_floor(x - lo, -delta), crawl_floor(x - cl, -delta)));
+    return true;
+}
+__device__ __forceinline__ Crawl crawl_steps(f3 on, f3 d, int32_t vx, int32_t vy, int32_t vz,
+                                             bool px, bool py, bool pz, uint32_t room) {
+    Crawl r{0u, 0.0f, 0.0f, 0.0f};
+    if (((f2i(on.x) ^ vx) | (f2i(on.y) ^ vy) | (f2i(on.z) ^ vz)) & ~7) return r;   // left the cluster
+    if (!(on.x >= 0.0f && on.y >= 0.0f && on.z >= 0.0f)) return r;
+    bool pinned = false;
+    float m = (float)room;
+    f3 dl{0.0f, 0.0f, 0.0f};
+    // one axis at a time (a rolled loop keeps its temporaries from stacking up
+    // on the walk's live registers: this cold block sets the kernel's VGPR count)
+#pragma unroll 1
+    for (uint32_t a = 0; a < 3u; ++a) {
+        float delta;
+        if (!crawl_axis(comp(on, a), comp(d, a), a == 0 ? vx : (a == 1 ? vy : vz), a == 0 ? px : (a == 1 ? py : pz),
+                        delta, pinned, m))
+            return r;
+        setf(dl, a, delta);
+    }
+    r.m = (pinned && m > 0.0f) ? (uint32_t)m : 0u;
+    r.dx = dl.x; r.dy = dl.y; r.dz = dl.z;
+    return r;
+}
+
+// CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
+// crawling ray reserves an entry in the launch's deferral list and unwinds.
+template <int STORE, bool COUNT, bool CRAWL>
 struct Walker : Ctx<STORE, COUNT> {
     using C = Ctx<STORE, COUNT>;
     using C::s; using C::v; using C::aborted; using C::tick; using C::exists; using C::lookup;
@@ -53,13 +123,6 @@ struct Walker : Ctx<STORE, COUNT> {
         float tZ = zz ? kInf : (nZ - o.z) / d.z;
         float tMin = fminf(tX, fminf(tY, tZ));
         o = add(o, scl(tMin + kEps, d));
-        // Hoisted reciprocals (div_fast) and +-1 plane signs for the loop.
-        const Rcp rx = rcp_setup(d.x), ry = rcp_setup(d.y), rz = rcp_setup(d.z);
-        const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
-        const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
-        // A guarded zero direction component (shadow ray) keeps the lane on the
-        // slow branch, which applies the guard: the fast path needs no selects.
-        const bool walk_ok = rx.ok && ry.ok && rz.ok && !zx && !zy && !zz;
         uint32_t col = kEmpty;
         if constexpr (STORE == STORE_VCS) {
             // Inside the region every voxel coordinate is in [0, 64): the mask
@@ -73,45 +136,114 @@ struct Walker : Ctx<STORE, COUNT> {
             // kept: iteration k of the pixel runs iff k <= kIterBudget.
             if (!this->in_region_bits(o)) return false;
             if (aborted || this->iters >= kIterBudget) { aborted = true; return false; }
-            bool found = false, inside = true;
+            bool found = false, inside = true, crawl = false;
+            // crawl exits (see crawl_steps): from this iteration count on (crawl pass);
+            // tile pass: until a deferral failed
+            uint32_t crawl_after = 0;
+            bool crawl_off = false;
             uint32_t vi = 0;
-            Blk blk;
+            int32_t qx = 0, qy = 0, qz = 0;   // voxel of the iteration that exited to crawl
             for (;;) {
-                ++this->iters;
-                const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-                this->count(4);
-                const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
-                blk = mreg[wi];
-                // both candidate planes, computed while the mask word is in
-                // flight and materialised (with the whole 8-B word: one load)
-                float vX = next_plane(o.x, gx, kEps), vY = next_plane(o.y, gy, kEps), vZ = next_plane(o.z, gz, kEps);
-                float cX = (float)((vx & ~7) + cx8), cY = (float)((vy & ~7) + cy8), cZ = (float)((vz & ~7) + cz8);
-                asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
-                const bool skip = absent(blk);
-                const uint32_t bit = (((uint32_t)vy & 3u) << 3) | ((uint32_t)vz & 7u);
-                found = (!skip) & (((blk.x >> bit) & 1u) != 0u);
-                vi = blk.y + __popc(blk.x & ((1u << bit) - 1u));
-                if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
-                nX = skip ? cX : vX;
-                nY = skip ? cY : vY;
-                nZ = skip ? cZ : vZ;
-                const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
-                float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
-                const bool bad = !walk_ok || !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= 0x1p-90f);
-                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                    sX = bad ? (zx ? kInf : ax / d.x) : sX;
-                    sY = bad ? (zy ? kInf : ay / d.y) : sY;
-                    sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                // Per-walk constants, (re)made here in the crawl pass so they are
+                // dead across the crawl code below (the barrier keeps them from
+                // being hoisted).
+                f3 dl = d;
+                if (CRAWL) asm("" : "+v"(dl.x), "+v"(dl.y), "+v"(dl.z));
+                // Hoisted reciprocals (div_fast) and +-1 plane signs for the loop.
+                const Rcp rx = rcp_setup(dl.x), ry = rcp_setup(dl.y), rz = rcp_setup(dl.z);
+                const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
+                const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
+                // A guarded zero direction component (shadow ray) keeps the lane on the
+                // slow branch, which applies the guard: the fast path needs no selects.
+                const bool walk_ok = rx.ok && ry.ok && rz.ok && !zx && !zy && !zz;
+                for (;;) {
+                    ++this->iters;
+                    const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
+                    this->count(4);
+                    const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
+                    Blk blk = mreg[wi];
+                    // both candidate planes, computed while the mask word is in
+                    // flight and materialised (with the whole 8-B word: one load)
+                    float vX = next_plane(o.x, gx, kEps), vY = next_plane(o.y, gy, kEps), vZ = next_plane(o.z, gz, kEps);
+                    float cX = (float)((vx & ~7) + cx8), cY = (float)((vy & ~7) + cy8), cZ = (float)((vz & ~7) + cz8);
+                    asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
+                    const bool skip = absent(blk);
+                    const uint32_t bit = (((uint32_t)vy & 3u) << 3) | ((uint32_t)vz & 7u);
+                    found = (!skip) & (((blk.x >> bit) & 1u) != 0u);
+                    vi = blk.y + __popc(blk.x & ((1u << bit) - 1u));
+                    if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
+                    nX = skip ? cX : vX;
+                    nY = skip ? cY : vY;
+                    nZ = skip ? cZ : vZ;
+                    const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
+                    float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
+                    const bool bad = !walk_ok || !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= 0x1p-90f);
+                    crawl = false;
+                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                        sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                        sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                        sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                        // a skip step with t = 0 (its plane axis has n = 0, so it is
+                        // always on this branch): the ray creeps through an empty cluster
+                        crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
+                                (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                    }
+                    const float sMin = fminf(sX, fminf(sY, sZ));
+                    const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
+                    tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
+                    const f3 on = add(o, scl(sMin + kEps, d));
+                    inside = this->in_region_bits(on);
+                    qx = vx; qy = vy; qz = vz;
+                    o.x = found ? o.x : on.x;   // per component: a struct-valued ?: goes through scratch
+                    o.y = found ? o.y : on.y;
+                    o.z = found ? o.z : on.z;
+                    if (found || !inside || this->iters >= kIterBudget || crawl) break;
                 }
-                const float sMin = fminf(sX, fminf(sY, sZ));
-                const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
-                tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
-                const f3 on = add(o, scl(sMin + kEps, d));
-                inside = this->in_region_bits(on);
-                o.x = found ? o.x : on.x;   // per component: a struct-valued ?: goes through scratch
-                o.y = found ? o.y : on.y;
-                o.z = found ? o.z : on.z;
-                if (found || !inside || this->iters >= kIterBudget) break;
+                if (!crawl || !inside || this->iters >= kIterBudget) break;
+                if constexpr (!CRAWL) {
+                    // Defer only a real crawl: an axis on its own skip plane that
+                    // EPSILON * d cannot move (it did not: o is the stepped position),
+                    // so t = 0 again and again.  A one-off t = 0 step walks on here.
+                    // (o on its plane (v & ~7) <=> o / 8 is an integer; o * 0.125 is exact)
+                    const bool kx = !px && truncf(o.x * 0.125f) == o.x * 0.125f && o.x + kEps * d.x == o.x;
+                    const bool ky = !py && truncf(o.y * 0.125f) == o.y * 0.125f && o.y + kEps * d.y == o.y;
+                    const bool kz = !pz && truncf(o.z * 0.125f) == o.z * 0.125f && o.z + kEps * d.z == o.z;
+                    // Defer the whole pixel to the crawl pass if a list entry is
+                    // free (unwinds like an abort); otherwise walk on plainly.
+                    if ((kx || ky || kz) && v.defer) {
+                        const uint32_t idx = atomicAdd(v.defer, 1u);
+                        if (idx < v.defer_cap) {
+                            // (the tile pass writes this pixel as 0; the crawl pass,
+                            // which runs after it, overwrites it and counts its bytes)
+                            const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+                            const uint32_t px_ = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
+                            const uint32_t pl_ = (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
+                            v.defer[2 + idx] = (pl_ << 16) | px_;
+                            if (COUNT) this->bytes = 0xFFFFFFFCu;     // + the final 4 = 0
+                            aborted = true;
+                            return false;
+                        }
+                    }
+                    if (kx || ky || kz) crawl_off = true;
+                } else {
+                    // Off the hot loop: fast-forward the identical crawl iterations
+                    // exactly, then resume the walk (no region-entry step).
+                    const Crawl cw = crawl_steps(o, d, qx, qy, qz, px, py, pz, kIterBudget - this->iters);
+                    // declined (binade edge, left the cluster, odd-mantissa tie): a few
+                    // plain iterations, then re-arm
+                    if (cw.m == 0u) {
+                        crawl_after = this->iters + 8u;
+                    } else {
+                        const float fm = (float)cw.m;       // exact: m * delta_i stays inside the binade
+                        o.x = o.x + fm * cw.dx;
+                        o.y = o.y + fm * cw.dy;
+                        o.z = o.z + fm * cw.dz;
+                        this->iters += cw.m;
+                        this->count(4u * cw.m);
+                        inside = this->in_region_bits(o);
+                        if (!inside || this->iters >= kIterBudget) break;
+                    }
+                }
             }
             if (!found) {
                 if (inside) aborted = true;     // the next iteration's tick() would have failed
@@ -119,6 +251,10 @@ struct Walker : Ctx<STORE, COUNT> {
             }
             col = s.vcs_vals[vi];
         } else {
+            const Rcp rx = rcp_setup(d.x), ry = rcp_setup(d.y), rz = rcp_setup(d.z);
+            const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
+            const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
+            const bool walk_ok = rx.ok && ry.ok && rz.ok && !zx && !zy && !zz;
             while (in_region(o)) {
                 if (!tick()) return false;
                 const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
@@ -369,49 +505,87 @@ struct Walker : Ctx<STORE, COUNT> {
     }
 };
 
-// rayMarchSceneOriginal / rayMarchSceneJumpAxis (Renderer.cuh:1033-1063).
+// The body of rayMarchSceneOriginal / rayMarchSceneJumpAxis (Renderer.cuh:1033-1063)
+// for pixel (x, local row l): colour, algorithmic bytes (+4 for the pixel write)
+// (a pixel deferred to the crawl pass comes back as 0 with 0 bytes).
+template <int STORE, int ALGO, bool COUNT, bool CRAWL>
+__device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, const float* inv255, uint32_t x, uint32_t l,
+                                          uint32_t& bytes) {
+    const uint32_t band = l / v.band_rows;
+    const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
+    uint32_t col = 0;
+    bytes = 0;
+    if (y < v.row_limit) {
+        // calculateWorldRay (Renderer.cuh:1013-1022) + Camera::generateRay (Camera.cuh:25-29)
+        float u = ((float)x + 0.5f) / (float)v.W;
+        float vv = ((float)(v.H - y) + 0.5f) / (float)v.H;
+        f3 ro = add(add(ld3(v.llc), scl(u, ld3(v.hor))), scl(vv, ld3(v.ver)));
+        f3 rd = unit(sub(ro, ld3(v.org)));
+        Walker<STORE, COUNT, CRAWL> w(s, v);
+        w.inv255 = inv255;
+        Hit h;
+        if (w.template primary<ALGO>(ro, rd, h)) {
+            bool sh = false;
+            // applyLighting (Renderer.cuh:249-258) at the hit; regionWorldPosition (:413)
+            const f3 rwp = add(ld3(v.translation), mk((float)(h.region.x * kBlock), (float)(h.region.y * kBlock),
+                                                      (float)(h.region.z * kBlock)));
+            const uint32_t lit = w.lighting(h.col, h.n, rwp, h.so);
+            if (v.use_shadows)
+                sh = h.longest ? w.template shadow<true>(h.so, h.region) : w.template shadow<false>(h.so, h.region);
+            col = lit * (uint32_t)!sh;
+        }
+        if (w.aborted) col = 0;
+        bytes = w.bytes + 4u;                     // + the pixel write
+    }
+    return col;
+}
+
+__device__ __forceinline__ void add_bytes(const KView& v, uint32_t lane, unsigned long long b) {
+    for (int off = 32; off > 0; off >>= 1) b += __shfl_down(b, off, 64);   // one atomic per wave
+    if (lane == 0 && b) atomicAdd(v.bytes, b);
+}
+
+// Tile pass: one lane per pixel, one wave per 8x8 tile, 2x2 tiles per workgroup.
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(256, ALGO == ALGO_ORIGINAL ? 7 : 3) void march_kernel(KScene s, KView v) {
     __shared__ float inv255_lds[256];
     const float* inv255 = load_inv255(inv255_lds);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t bx = blockIdx.x, by = blockIdx.y;
-    const uint32_t x = (bx * 2u + (wave & 1u)) * 8u + (lane & 7u);
-    const uint32_t l = (by * 2u + (wave >> 1)) * 8u + (lane >> 3);
+    const uint32_t x = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
+    const uint32_t l = (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
     uint32_t bytes = 0;
     if (x < v.W && l < v.local_rows) {
-        const uint32_t band = l / v.band_rows;
-        const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
-        uint32_t col = 0;
-        if (y < v.row_limit) {
-            // calculateWorldRay (Renderer.cuh:1013-1022) + Camera::generateRay (Camera.cuh:25-29)
-            float u = ((float)x + 0.5f) / (float)v.W;
-            float vv = ((float)(v.H - y) + 0.5f) / (float)v.H;
-            f3 ro = add(add(ld3(v.llc), scl(u, ld3(v.hor))), scl(vv, ld3(v.ver)));
-            f3 rd = unit(sub(ro, ld3(v.org)));
-            Walker<STORE, COUNT> w(s, v);
-            w.inv255 = inv255;
-            Hit h;
-            if (w.template primary<ALGO>(ro, rd, h)) {
-                bool sh = false;
-                // applyLighting (Renderer.cuh:249-258) at the hit; regionWorldPosition (:413)
-                const f3 rwp = add(ld3(v.translation), mk((float)(h.region.x * kBlock), (float)(h.region.y * kBlock),
-                                                          (float)(h.region.z * kBlock)));
-                const uint32_t lit = w.lighting(h.col, h.n, rwp, h.so);
-                if (v.use_shadows)
-                    sh = h.longest ? w.template shadow<true>(h.so, h.region) : w.template shadow<false>(h.so, h.region);
-                col = lit * (uint32_t)!sh;
-            }
-            if (w.aborted) col = 0;
-            bytes = w.bytes + 4u;                 // + the pixel write
-        }
-        v.out[(size_t)l * v.W + x] = col;
+        __builtin_nontemporal_store(shade<STORE, ALGO, COUNT, false>(s, v, inv255, x, l, bytes), &v.out[(size_t)l * v.W + x]);
     }
-    if (COUNT) {
-        // wave64 reduction, one atomic per wave
-        unsigned long long b = bytes;
-        for (int off = 32; off > 0; off >>= 1) b += __shfl_down(b, off, 64);
-        if (lane == 0 && b) atomicAdd(v.bytes, b);
+    if (COUNT) add_bytes(v, lane, bytes);
+}
+
+// Crawl pass: the deferred pixels of this launch, one per lane, with the
+// exact crawl fast-forward; the last workgroup resets the slot for reuse.
+template <int STORE, int ALGO, bool COUNT>
+__global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
+    __shared__ float inv255_lds[256];
+    __shared__ uint32_t n_lds;
+    if (threadIdx.x == 0) n_lds = v.defer[0];
+    __syncthreads();
+    const uint32_t total = n_lds;
+    if (total == 0u) return;                  // nothing deferred (the usual case): no reset needed
+    const uint32_t n = min(total, v.defer_cap);
+    const float* inv255 = load_inv255(inv255_lds);
+    unsigned long long bytes = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t e = v.defer[2 + i], x = e & 0xFFFFu, l = e >> 16;
+        uint32_t b;
+        __builtin_nontemporal_store(shade<STORE, ALGO, COUNT, true>(s, v, inv255, x, l, b), &v.out[(size_t)l * v.W + x]);
+        bytes += b;
+    }
+    if (COUNT) add_bytes(v, threadIdx.x & 63u, bytes);
+    // Every workgroup has read the count (above) before it adds to `done`; the
+    // last one clears the slot for its next launch (ordered by the kernel boundary).
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(&v.defer[1], 1u) == gridDim.x - 1u) {
+        v.defer[0] = 0;
+        v.defer[1] = 0;
     }
 }
 
@@ -430,7 +604,14 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
     dim3 grid((v.W + 15u) / 16u, (v.local_rows + 15u) / 16u);
     dim3 block(256);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-#define VR_LAUNCH(ST, AL, CT) hipLaunchKernelGGL((march_kernel<ST, AL, CT>), grid, block, 0, stream, s, v)
+    // VCS walks can crawl: a small crawl-pass grid follows the tile pass
+    // (it exits at once when nothing was deferred).
+    const dim3 cgrid(64);
+#define VR_LAUNCH(ST, AL, CT)                                                                     \
+    do {                                                                                           \
+        hipLaunchKernelGGL((march_kernel<ST, AL, CT>), grid, block, 0, stream, s, v);              \
+        if (ST == STORE_VCS && v.defer) hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, block, 0, stream, s, v); \
+    } while (0)
     if (store == STORE_VCS) {
         if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, false); }
         else { if (count) VR_LAUNCH(STORE_VCS, ALGO_LONGEST, true); else VR_LAUNCH(STORE_VCS, ALGO_LONGEST, false); }
