@@ -555,7 +555,7 @@ __global__ __launch_bounds__(256, ALGO == ALGO_ORIGINAL ? 7 : 3) void march_kern
     const uint32_t l = (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
     uint32_t bytes = 0;
     if (x < v.W && l < v.local_rows) {
-        __builtin_nontemporal_store(shade<STORE, ALGO, COUNT, false>(s, v, inv255, x, l, bytes), &v.out[(size_t)l * v.W + x]);
+        v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, false>(s, v, inv255, x, l, bytes);
     }
     if (COUNT) add_bytes(v, lane, bytes);
 }
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t e = v.defer[2 + i], x = e & 0xFFFFu, l = e >> 16;
         uint32_t b;
-        __builtin_nontemporal_store(shade<STORE, ALGO, COUNT, true>(s, v, inv255, x, l, b), &v.out[(size_t)l * v.W + x]);
+        v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, true>(s, v, inv255, x, l, b);
         bytes += b;
     }
     if (COUNT) add_bytes(v, threadIdx.x & 63u, bytes);
