@@ -97,7 +97,9 @@ int vr_scene_create(int device, vr_store store, const int32_t* xyz, const uint32
                     size_t n, vr_scene** out);
 
 /* VoxelFile::readVoxelFile (geometry/VoxelFile.cuh:9-35) + vr_scene_create.
- * Unlike the reference the path is used as given (no "resources/" prefix). */
+ * Unlike the reference the path is used as given (no "resources/" prefix).
+ * Accepts the .vox CSV (parsed in parallel, same rules and first-error line)
+ * or the .vxb binary sidecar (detected by its magic). */
 int vr_scene_load_vox(int device, vr_store store, const char* path, vr_scene** out);
 
 int vr_scene_get_info(const vr_scene* s, vr_scene_info* out);
@@ -171,6 +173,14 @@ int vr_synth_generate(const vr_synth_params* p, int32_t* xyz, uint32_t* rgb, siz
  * Reader: two-phase like vr_synth_generate. */
 int vr_vox_read(const char* path, int32_t* xyz, uint32_t* rgb, size_t capacity, size_t* n_out);
 int vr_vox_write(const char* path, const int32_t* xyz, const uint32_t* rgb, size_t n);
+
+/* .vxb binary scene sidecar: 32-byte header {"VRVXB001",
+ * u64 count, u64 reserved[2]}, then int32 xyz[3*count], uint32 rgb[count]
+ * (little endian, insertion order).  Same two-call protocol as vr_vox_read. */
+int vr_vxb_read(const char* path, int32_t* xyz, uint32_t* rgb, size_t capacity, size_t* n_out);
+int vr_vxb_write(const char* path, const int32_t* xyz, const uint32_t* rgb, size_t n);
+/* Either format, detected by the .vxb magic. */
+int vr_scene_file_read(const char* path, int32_t* xyz, uint32_t* rgb, size_t capacity, size_t* n_out);
 
 const char* vr_last_error(void);
 const char* vr_version(void);

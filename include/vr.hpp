@@ -101,13 +101,23 @@ private:
 };
 
 struct VoxelFile {
+    // .vox CSV or, detected by its magic, the .vxb binary sidecar.
     static void readVoxelFile(VoxelSceneCPU& scene, const std::string& path) {
         size_t n = 0;
-        check(vr_vox_read(path.c_str(), nullptr, nullptr, 0, &n), "readVoxelFile");
+        check(vr_scene_file_read(path.c_str(), nullptr, nullptr, 0, &n), "readVoxelFile");
         std::vector<int32_t> xyz(3 * n + 3);
         std::vector<uint32_t> rgb(n + 1);
-        check(vr_vox_read(path.c_str(), xyz.data(), rgb.data(), n, &n), "readVoxelFile");
+        check(vr_scene_file_read(path.c_str(), xyz.data(), rgb.data(), n, &n), "readVoxelFile");
         for (size_t i = 0; i < n; ++i) scene.insertVoxel(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], rgb[i]);
+    }
+    // Write the binary sidecar of a scene file (vr_vxb_write).
+    static void writeBinary(const std::string& src, const std::string& dst) {
+        size_t n = 0;
+        check(vr_scene_file_read(src.c_str(), nullptr, nullptr, 0, &n), "readVoxelFile");
+        std::vector<int32_t> xyz(3 * n + 3);
+        std::vector<uint32_t> rgb(n + 1);
+        check(vr_scene_file_read(src.c_str(), xyz.data(), rgb.data(), n, &n), "readVoxelFile");
+        check(vr_vxb_write(dst.c_str(), xyz.data(), rgb.data(), n), "vr_vxb_write");
     }
 };
 

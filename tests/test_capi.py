@@ -139,3 +139,62 @@ def test_cli_binary_built():
     assert os.access(exe, os.X_OK)
     out = os.popen(f"{exe} --help").read()
     assert "hashtable|vcs" in out
+
+
+def test_cli_converts_scene_to_vxb(tmp_path):
+    exe = os.path.join(ROOT, "voxelraymarcher_amd", "bin", "VoxelRaymarcher")
+    xyz, rgb = vr.CONFIGS["C1"].voxels()
+    src, dst = str(tmp_path / "scene.vox"), str(tmp_path / "scene.vxb")
+    vr.write_voxel_file(src, xyz, rgb)
+    assert os.system(f"{exe} --scene {src} --write-vxb {dst} > /dev/null") == 0
+    a, b = vr.read_voxel_file(dst)
+    assert np.array_equal(a, xyz) and np.array_equal(b, rgb)
+
+
+def test_binary_scene_roundtrip_and_detection(tmp_path):
+    """.vxb sidecar: same voxels, same order, auto-detected."""
+    rng = np.random.default_rng(7)
+    xyz = rng.integers(-300, 300, size=(5000, 3)).astype(np.int32)
+    rgb = rng.integers(0, 1 << 24, size=5000).astype(np.uint32)
+    xyz[17] = xyz[3]                        # a duplicate: order must survive
+    p = str(tmp_path / "scene.vxb")
+    vr.write_binary_scene(p, xyz, rgb)
+    a, b = vr.read_voxel_file(p)
+    assert np.array_equal(a, xyz) and np.array_equal(b, rgb)
+    q = str(tmp_path / "empty.vxb")
+    vr.write_binary_scene(q, np.zeros((0, 3), np.int32), np.zeros(0, np.uint32))
+    a, b = vr.read_voxel_file(q)
+    assert a.shape == (0, 3) and b.shape == (0,)
+    bad = str(tmp_path / "trunc.vxb")
+    open(bad, "wb").write(open(p, "rb").read()[:1000])
+    with pytest.raises(vr.VrError) as e:
+        vr.read_voxel_file(bad)
+    assert e.value.code == -6
+
+
+def test_parallel_csv_parse_matches_python(tmp_path):
+    """A multi-MB .vox is split across threads: voxels in file order and the
+    first error's line number exactly as a sequential reading gives them."""
+    rng = np.random.default_rng(11)
+    n = 400_000
+    xyz = rng.integers(-2000, 2000, size=(n, 3)).astype(np.int32)
+    rgb = rng.integers(0, 1 << 24, size=n).astype(np.uint32)
+    lines = [f"{x},{y},{z},{c}" for (x, y, z), c in zip(xyz.tolist(), rgb.tolist())]
+    # sprinkle ignorable lines and odd-but-valid forms at chunk-boundary-ish places
+    for i in (0, 1, n // 7, n // 3, n // 2, n - 1):
+        lines.insert(i, "")
+    lines.insert(n // 5, "1,2")
+    lines.insert(n // 4, ",,9,,8,,7,,6,")
+    p = str(tmp_path / "big.vox")
+    open(p, "w").write("\n".join(lines) + "\n")
+    a, b = vr.read_voxel_file(p)
+    want = [[int(t) for t in l.replace(",", " ").split()] for l in lines if len([t for t in l.split(",") if t]) > 3]
+    assert a.shape[0] == len(want)
+    assert np.array_equal(a, np.array([w[:3] for w in want], np.int32))
+    assert np.array_equal(b, np.array([w[3] for w in want], np.uint32))
+    bad_at = 300_000
+    lines[bad_at] = "1,2,zz,4"
+    open(p, "w").write("\n".join(lines) + "\n")
+    with pytest.raises(vr.VrError) as e:
+        vr.read_voxel_file(p)
+    assert e.value.code == -6 and f":{bad_at + 1}:" in str(e.value)

@@ -11,9 +11,9 @@ from ._capi import LIB_PATH, VrError, lib
 from .renderer import (CONFIGS, Camera, DeviceScene, Kernel, render_ex, RayMarchAlgorithm, RenderConfig, StorageType, VoxelSceneCPU,
                        VoxelSceneInfo, band_buffer_words, create_scene, pack_rgb8, parse_algorithm, parse_storage,
                        read_voxel_file, render_bands, render_count, run_raymarching_kernel, setup_constant_values,
-                       synth_scene, write_voxel_file)
+                       synth_scene, write_binary_scene, write_voxel_file)
 
 __all__ = ["LIB_PATH", "VrError", "lib", "CONFIGS", "Camera", "DeviceScene", "Kernel", "render_ex", "RayMarchAlgorithm", "RenderConfig",
            "StorageType", "VoxelSceneCPU", "VoxelSceneInfo", "band_buffer_words", "create_scene", "pack_rgb8",
            "parse_algorithm", "parse_storage", "read_voxel_file", "render_bands", "render_count",
-           "run_raymarching_kernel", "setup_constant_values", "synth_scene", "write_voxel_file"]
+           "run_raymarching_kernel", "setup_constant_values", "synth_scene", "write_binary_scene", "write_voxel_file"]

@@ -85,6 +85,9 @@ SIGNATURES = {
                                   POINTER(c_size_t)]),
     "vr_vox_read": (c_int, [c_char_p, POINTER(c_int32), POINTER(c_uint32), c_size_t, POINTER(c_size_t)]),
     "vr_vox_write": (c_int, [c_char_p, POINTER(c_int32), POINTER(c_uint32), c_size_t]),
+    "vr_vxb_read": (c_int, [c_char_p, POINTER(c_int32), POINTER(c_uint32), c_size_t, POINTER(c_size_t)]),
+    "vr_vxb_write": (c_int, [c_char_p, POINTER(c_int32), POINTER(c_uint32), c_size_t]),
+    "vr_scene_file_read": (c_int, [c_char_p, POINTER(c_int32), POINTER(c_uint32), c_size_t, POINTER(c_size_t)]),
     "vr_last_error": (c_char_p, []),
     "vr_version": (c_char_p, []),
 }

@@ -3,6 +3,7 @@
 //   VoxelRaymarcher [scale] {hashtable|vcs} {original|longestaxis}
 //                   [--scene resources/scene.vox] [--width 1920] [--height 1080]
 //                   [--out output.png] [--device 0] [--synth N] [--repeat K]
+//                   [--write-vxb F]   (convert the scene to the .vxb sidecar and exit)
 // Defaults follow Main.cu: VCS unless "hashtable", longest axis unless
 // "original" (:45-68), 1920x1080 (:195-196), camera (6,2,6)->(0,0,-1) fov 60
 // (:199), translation 0 (:215), scene file resources/scene.vox (:96-103).
@@ -85,7 +86,7 @@ bool write_png(const char* path, const uint8_t* rgb, uint32_t w, uint32_t h) {
 
 int main(int argc, char* argv[]) {
     std::vector<const char*> pos;
-    std::string scene_path = "resources/scene.vox", out_path = "output.png";
+    std::string scene_path = "resources/scene.vox", out_path = "output.png", vxb_path;
     uint32_t width = 1920, height = 1080, synth = 0;
     int device = 0, repeat = 1;
     for (int i = 1; i < argc; ++i) {
@@ -101,11 +102,22 @@ int main(int argc, char* argv[]) {
         else if (a == "--device") device = std::atoi(next("--device"));
         else if (a == "--synth") synth = (uint32_t)std::strtoul(next("--synth"), nullptr, 10);
         else if (a == "--repeat") repeat = std::max(1, std::atoi(next("--repeat")));
+        else if (a == "--write-vxb") vxb_path = next("--write-vxb");
         else if (a == "-h" || a == "--help") {
             std::cout << "usage: VoxelRaymarcher [scale] {hashtable|vcs} {original|longestaxis} [--scene F] "
-                         "[--width W] [--height H] [--out F] [--device N] [--synth N] [--repeat K]" << std::endl;
+                         "[--width W] [--height H] [--out F] [--device N] [--synth N] [--repeat K] [--write-vxb F]" << std::endl;
             return 0;
         } else pos.push_back(argv[i]);
+    }
+    if (!vxb_path.empty()) {                 // scene conversion only: no GPU needed
+        try {
+            vrx::VoxelFile::writeBinary(scene_path, vxb_path);
+        } catch (const vrx::Error& e) {
+            std::cerr << e.what() << std::endl;
+            return 1;
+        }
+        std::cout << "wrote " << vxb_path << std::endl;
+        return 0;
     }
     // argv[1] = scale (Main.cu:181-186); optional here (README.md:22-25 omits it).
     uint32_t scale = 1;

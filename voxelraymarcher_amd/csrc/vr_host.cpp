@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "vr.h"
@@ -484,6 +485,141 @@ bool stoi_like(const char* b, const char* e, int32_t* out) {
     return true;
 }
 
+// Whole-file read (the .vox parser splits the text across threads).
+int read_file(const char* path, std::vector<char>& out) {
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(VR_E_IO, std::string("cannot open ") + path + ": " + std::strerror(errno));
+    char buf[1 << 16];
+    size_t got;
+    while ((got = std::fread(buf, 1, sizeof buf, f)) > 0) out.insert(out.end(), buf, buf + got);
+    const bool err = std::ferror(f) != 0;
+    std::fclose(f);
+    if (err) return fail(VR_E_IO, std::string("read failed: ") + path);
+    return VR_OK;
+}
+
+// VoxelFile::readVoxelFile (VoxelFile.cuh:11-35) for one line: comma-separated
+// fields with empty fields skipped (find_first_not_of(",")), lines with <= 3
+// fields ignored, each of the first four fields converted like std::stoi.
+// Returns 1 = voxel, 0 = ignored line, -1 = std::stoi would throw.
+int parse_vox_line(const char* p, const char* e, int32_t v[4]) {
+    const char* fb[4] = {nullptr, nullptr, nullptr, nullptr};
+    const char* fe[4] = {nullptr, nullptr, nullptr, nullptr};
+    int nf = 0;
+    while (p < e) {
+        while (p < e && *p == ',') ++p;
+        if (p >= e) break;
+        const char* q = p;
+        while (q < e && *q != ',') ++q;
+        if (nf < 4) { fb[nf] = p; fe[nf] = q; }
+        ++nf;
+        p = q;
+    }
+    if (nf <= 3) return 0;                     // lineEntries.size() > 3 (VoxelFile.cuh:25)
+    for (int i = 0; i < 4; ++i)
+        if (!stoi_like(fb[i], fe[i], &v[i])) return -1;
+    return 1;
+}
+
+struct VoxParse {
+    std::vector<int32_t> xyz;
+    std::vector<uint32_t> rgb;
+};
+
+// The text is cut at newlines into one chunk per worker; chunks are parsed in
+// parallel and concatenated in file order (later duplicates must stay later).
+// The first error in file order is reported with its line number.
+int parse_vox_text(const char* path, const std::vector<char>& text, VoxParse& out) {
+    const size_t len = text.size();
+    const char* base = text.data();
+    unsigned hw = std::thread::hardware_concurrency();
+    size_t workers = std::max<size_t>(1, std::min<size_t>({(size_t)(hw ? hw : 1), (size_t)16, len / (1u << 20) + 1}));
+    std::vector<size_t> cut(workers + 1, len);
+    cut[0] = 0;
+    for (size_t w = 1; w < workers; ++w) {
+        size_t c = std::max(cut[w - 1], len * w / workers);
+        while (c < len && base[c - 1] != '\n') ++c;
+        cut[w] = c;
+    }
+    struct Part {
+        VoxParse vp;
+        size_t lines = 0;            // newline-terminated or final lines seen
+        size_t bad_line = 0;         // 1-based within the chunk, 0 = none
+    };
+    std::vector<Part> parts(workers);
+    auto run = [&](size_t w) {
+        Part& pt = parts[w];
+        const char* p = base + cut[w];
+        const char* end = base + cut[w + 1];
+        pt.vp.xyz.reserve((size_t)(end - p) / 8 * 3);
+        pt.vp.rgb.reserve((size_t)(end - p) / 24);
+        while (p < end) {
+            const char* q = (const char*)std::memchr(p, '\n', (size_t)(end - p));
+            const char* le = q ? q : end;
+            ++pt.lines;
+            int32_t v[4];
+            const int r = parse_vox_line(p, le, v);
+            if (r < 0) { pt.bad_line = pt.lines; return; }
+            if (r > 0) {
+                pt.vp.xyz.insert(pt.vp.xyz.end(), {v[0], v[1], v[2]});
+                pt.vp.rgb.push_back((uint32_t)v[3]);
+            }
+            p = q ? q + 1 : end;
+        }
+    };
+    if (workers == 1) {
+        run(0);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t w = 0; w < workers; ++w) th.emplace_back(run, w);
+        for (auto& t : th) t.join();
+    }
+    size_t line0 = 0, n = 0;
+    for (size_t w = 0; w < workers; ++w) {
+        if (parts[w].bad_line) {
+            // lines before this chunk: every earlier chunk ends with a newline
+            return fail(VR_E_PARSE, std::string(path) + ":" + std::to_string(line0 + parts[w].bad_line) +
+                                        ": std::stoi would throw");
+        }
+        line0 += parts[w].lines;
+        n += parts[w].vp.rgb.size();
+    }
+    out.xyz.reserve(3 * n);
+    out.rgb.reserve(n);
+    for (auto& pt : parts) {
+        out.xyz.insert(out.xyz.end(), pt.vp.xyz.begin(), pt.vp.xyz.end());
+        out.rgb.insert(out.rgb.end(), pt.vp.rgb.begin(), pt.vp.rgb.end());
+    }
+    return VR_OK;
+}
+
+// .vxb: the binary scene sidecar -- 32-byte header {"VRVXB001", u64 count,
+// u64 reserved x2}, then int32 xyz[3 * count] and uint32 rgb[count], little
+// endian, in insertion order (duplicates resolve exactly as in the CSV).
+constexpr char kVxbMagic[9] = "VRVXB001";
+struct VxbHeader {
+    char magic[8];
+    uint64_t count = 0;
+    uint64_t reserved[2] = {0, 0};
+};
+static_assert(sizeof(VxbHeader) == 32, "vxb header");
+
+int read_vxb_header(FILE* f, const char* path, VxbHeader& hd) {
+    if (std::fread(&hd, sizeof hd, 1, f) != 1 || std::memcmp(hd.magic, kVxbMagic, 8) != 0)
+        return fail(VR_E_PARSE, std::string(path) + ": not a .vxb scene (bad header)");
+    if (hd.count >= 0xFFFFFFFFull) return fail(VR_E_PARSE, std::string(path) + ": .vxb voxel count too large");
+    return VR_OK;
+}
+
+bool is_vxb(const char* path) {
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return false;
+    char m[8];
+    const bool yes = std::fread(m, 1, 8, f) == 8 && std::memcmp(m, kVxbMagic, 8) == 0;
+    std::fclose(f);
+    return yes;
+}
+
 }  // namespace
 
 extern "C" {
@@ -525,14 +661,25 @@ int vr_scene_create(int device, vr_store store, const int32_t* xyz, const uint32
 }
 
 int vr_scene_load_vox(int device, vr_store store, const char* path, vr_scene** out) {
-    size_t n = 0;
-    int rc = vr_vox_read(path, nullptr, nullptr, 0, &n);
+    if (!path) return fail(VR_E_INVALID, "NULL argument");
+    if (is_vxb(path)) {
+        size_t n = 0;
+        int rc = vr_vxb_read(path, nullptr, nullptr, 0, &n);
+        if (rc) return rc;
+        std::vector<int32_t> xyz(3 * n + 3);
+        std::vector<uint32_t> rgb(n + 1);
+        rc = vr_vxb_read(path, xyz.data(), rgb.data(), n, &n);
+        if (rc) return rc;
+        return build_scene(device, store, xyz.data(), rgb.data(), n, out);
+    }
+    std::vector<char> text;                 // CSV: read and parse once
+    int rc = read_file(path, text);
     if (rc) return rc;
-    std::vector<int32_t> xyz(3 * n + 3);
-    std::vector<uint32_t> rgb(n + 1);
-    rc = vr_vox_read(path, xyz.data(), rgb.data(), n, &n);
+    VoxParse vp;
+    rc = parse_vox_text(path, text, vp);
     if (rc) return rc;
-    return build_scene(device, store, xyz.data(), rgb.data(), n, out);
+    std::vector<char>().swap(text);
+    return build_scene(device, store, vp.xyz.data(), vp.rgb.data(), vp.rgb.size(), out);
 }
 
 int vr_scene_get_info(const vr_scene* s, vr_scene_info* out) {
@@ -648,54 +795,62 @@ int vr_synth_generate(const vr_synth_params* p, int32_t* xyz, uint32_t* rgb, siz
 
 int vr_vox_read(const char* path, int32_t* xyz, uint32_t* rgb, size_t capacity, size_t* n_out) {
     if (!path || !n_out) return fail(VR_E_INVALID, "NULL argument");
+    std::vector<char> text;
+    int rc = read_file(path, text);
+    if (rc) return rc;
+    VoxParse vp;
+    rc = parse_vox_text(path, text, vp);
+    if (rc) return rc;
+    const size_t n = vp.rgb.size();
+    if (xyz) {
+        if (!rgb) return fail(VR_E_INVALID, "rgb NULL");
+        if (n > capacity) return fail(VR_E_INVALID, "capacity too small");
+        std::memcpy(xyz, vp.xyz.data(), 3 * n * sizeof(int32_t));
+        std::memcpy(rgb, vp.rgb.data(), n * sizeof(uint32_t));
+    }
+    *n_out = n;
+    return VR_OK;
+}
+
+int vr_vxb_read(const char* path, int32_t* xyz, uint32_t* rgb, size_t capacity, size_t* n_out) {
+    if (!path || !n_out) return fail(VR_E_INVALID, "NULL argument");
     FILE* f = std::fopen(path, "rb");
     if (!f) return fail(VR_E_IO, std::string("cannot open ") + path + ": " + std::strerror(errno));
-    std::string line;
-    size_t cnt = 0, lineno = 0;
-    char buf[1 << 16];
-    int rc = VR_OK;
-    auto process = [&](const std::string& ln) -> int {
-        ++lineno;
-        // Destructure comma separated values, skipping empty fields (find_first_not_of(",")).
-        const char* p = ln.data();
-        const char* e = p + ln.size();
-        const char* fb[4] = {nullptr, nullptr, nullptr, nullptr};
-        const char* fe[4] = {nullptr, nullptr, nullptr, nullptr};
-        int nf = 0;
-        while (p < e) {
-            while (p < e && *p == ',') ++p;
-            if (p >= e) break;
-            const char* q = p;
-            while (q < e && *q != ',') ++q;
-            if (nf < 4) { fb[nf] = p; fe[nf] = q; }
-            ++nf;
-            p = q;
-        }
-        if (nf <= 3) return VR_OK;                  // lineEntries.size() > 3 (VoxelFile.cuh:25)
-        int32_t v[4];
-        for (int i = 0; i < 4; ++i)
-            if (!stoi_like(fb[i], fe[i], &v[i]))
-                return fail(VR_E_PARSE, std::string(path) + ":" + std::to_string(lineno) + ": std::stoi would throw");
-        if (xyz) {
-            if (cnt >= capacity) return fail(VR_E_INVALID, "capacity too small");
-            xyz[3 * cnt] = v[0]; xyz[3 * cnt + 1] = v[1]; xyz[3 * cnt + 2] = v[2];
-            rgb[cnt] = (uint32_t)v[3];
-        }
-        ++cnt;
-        return VR_OK;
-    };
-    size_t got;
-    while ((got = std::fread(buf, 1, sizeof buf, f)) > 0 && rc == VR_OK) {
-        for (size_t i = 0; i < got && rc == VR_OK; ++i) {
-            if (buf[i] == '\n') { rc = process(line); line.clear(); }
-            else line.push_back(buf[i]);
+    VxbHeader hd;
+    int rc = read_vxb_header(f, path, hd);
+    if (rc) { std::fclose(f); return rc; }
+    if (xyz) {
+        if (!rgb) { std::fclose(f); return fail(VR_E_INVALID, "rgb NULL"); }
+        if (hd.count > capacity) { std::fclose(f); return fail(VR_E_INVALID, "capacity too small"); }
+        if (std::fread(xyz, sizeof(int32_t), 3 * (size_t)hd.count, f) != 3 * (size_t)hd.count ||
+            std::fread(rgb, sizeof(uint32_t), (size_t)hd.count, f) != (size_t)hd.count) {
+            std::fclose(f);
+            return fail(VR_E_PARSE, std::string(path) + ": truncated .vxb payload");
         }
     }
-    if (rc == VR_OK && !line.empty()) rc = process(line);
     std::fclose(f);
-    if (rc) return rc;
-    *n_out = cnt;
+    *n_out = (size_t)hd.count;
     return VR_OK;
+}
+
+int vr_vxb_write(const char* path, const int32_t* xyz, const uint32_t* rgb, size_t n) {
+    if (!path || (n && (!xyz || !rgb))) return fail(VR_E_INVALID, "NULL argument");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(VR_E_IO, std::string("cannot open ") + path + ": " + std::strerror(errno));
+    VxbHeader hd;
+    std::memcpy(hd.magic, kVxbMagic, 8);
+    hd.count = n;
+    bool ok = std::fwrite(&hd, sizeof hd, 1, f) == 1 &&
+              (n == 0 || (std::fwrite(xyz, sizeof(int32_t), 3 * n, f) == 3 * n &&
+                          std::fwrite(rgb, sizeof(uint32_t), n, f) == n));
+    if (std::fclose(f) != 0) ok = false;
+    if (!ok) return fail(VR_E_IO, std::string("write failed: ") + path);
+    return VR_OK;
+}
+
+int vr_scene_file_read(const char* path, int32_t* xyz, uint32_t* rgb, size_t capacity, size_t* n_out) {
+    if (!path) return fail(VR_E_INVALID, "NULL argument");
+    return is_vxb(path) ? vr_vxb_read(path, xyz, rgb, capacity, n_out) : vr_vox_read(path, xyz, rgb, capacity, n_out);
 }
 
 int vr_vox_write(const char* path, const int32_t* xyz, const uint32_t* rgb, size_t n) {

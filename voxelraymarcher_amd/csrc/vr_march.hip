@@ -292,154 +292,148 @@ struct Walker : Ctx<STORE, COUNT> {
         return true;
     }
 
-    // State of one longest-axis region walk (Renderer.cuh:760-915 / :495-631).
-    struct LA {
-        f3 old_o, ray_o, ds;
-        i3 g, ad;
-        uint32_t L, M, S;
-    };
-
-    // performVoxelSpaceJump (Renderer.cuh:696-751) / performShadowVoxelSpaceJump (:441-492).
-    // Returns 0 = EMPTY_VAL (left region / aborted), 1 = hit, 2 = CONTINUE_VAL.
-    template <bool SHADOW>
-    __device__ __forceinline__ int jump(f3& oo, LA& a, uint32_t reg, i3 cr, Hit& h) {
-        float tX = 0.0f, tY = 0.0f, tZ = 0.0f, tMin = 0.0f;
-        Blk blk;
-        while (absent(blk = exists(reg, a.g.x, a.g.y, a.g.z))) {
-            if (!tick()) return 0;
-            int32_t nx = a.ds.x > 0.0f ? ((a.g.x / 8) + 1) * 8 : (a.g.x / 8) * 8;
-            int32_t ny = a.ds.y > 0.0f ? ((a.g.y / 8) + 1) * 8 : (a.g.y / 8) * 8;
-            int32_t nz = a.ds.z > 0.0f ? ((a.g.z / 8) + 1) * 8 : (a.g.z / 8) * 8;
-            tX = ((float)nx - a.old_o.x) / a.ds.x;
-            tY = ((float)ny - a.old_o.y) / a.ds.y;
-            tZ = ((float)nz - a.old_o.z) / a.ds.z;
-            tMin = fminf(tX, fminf(tY, tZ)) + kEps;
-            a.old_o = add(a.old_o, scl(tMin, a.ds));
-            a.g = i3{f2i(floorf(a.old_o.x)), f2i(floorf(a.old_o.y)), f2i(floorf(a.old_o.z))};
-            if (!grid_in_region(a.g.x, a.g.y, a.g.z)) {
-                oo = a.old_o;
-                return 0;
-            }
-        }
-        uint32_t col = lookup(reg, blk, a.g.x, a.g.y, a.g.z);
-        if (col != kEmpty) {
-            if (!SHADOW) {
-                h.col = col;
-                h.n = normal_from_t(tX, tY, tZ, tMin, a.ds);
-                h.so = a.old_o;
-                h.region = cr;
-                h.longest = true;
-            }
-            return 1;
-        }
-        float oL = comp(a.old_o, a.L), dL = comp(a.ds, a.L);
-        float tNext = dL > 0.0f ? (ceilf(oL) - oL) / dL : (floorf(oL) - oL) / dL;
-        a.ray_o = add(a.old_o, scl(tNext + kEps, a.ds));
-        seti(a.ad, a.M, f2i(comp(a.ray_o, a.M)) - geti(a.g, a.M));
-        seti(a.ad, a.S, f2i(comp(a.ray_o, a.S)) - geti(a.g, a.S));
-        return 2;
-    }
-
-    // One "grid += diff; exists? else jump; lookup; hit" block
-    // (Renderer.cuh:807-901 / :542-617).  0 = go on, 1 = return *res, 2 = continue.
-    template <bool SHADOW>
-    __device__ __forceinline__ int axis_step(f3& oo, LA& a, uint32_t axis, bool long_axis, uint32_t reg, i3 cr,
-                             Hit& h, bool& res) {
-        seti(a.g, axis, geti(a.g, axis) + geti(a.ad, axis));
-        Blk blk = exists(reg, a.g.x, a.g.y, a.g.z);
-        if (absent(blk)) {
-            int jr = jump<SHADOW>(oo, a, reg, cr, h);
-            if (aborted) { res = false; return 1; }
-            if (jr != 2) { res = jr == 1; return 1; }
-            return 2;
-        }
-        uint32_t col = lookup(reg, blk, a.g.x, a.g.y, a.g.z);
-        if (col != kEmpty) {
-            if (!SHADOW) {
-                f3 n = mk(0.0f, 0.0f, 0.0f);
-                setf(n, axis, copysignf(1.0f, -comp(a.ds, axis)));
-                f3 hit;
-                if (long_axis) {
-                    hit = a.ray_o;
-                } else {  // getLocalHitLocation (Renderer.cuh:753-758)
-                    float o = comp(a.old_o, axis), dd = comp(a.ds, axis);
-                    float t = dd > 0.0f ? (ceilf(o) - o) / dd : (floorf(o) - o) / dd;
-                    hit = add(a.old_o, scl(t, a.ds));
-                }
-                h.col = col;
-                h.n = n;
-                h.so = hit;
-                h.region = cr;
-                h.longest = true;
-            }
-            res = true;
-            return 1;
-        }
-        return 0;
-    }
-
-    // rayMarchVoxelGridLongestAxis (Renderer.cuh:760-915) /
-    // shadowRayMarchVoxelGridLongestAxis (:495-631).
+    // rayMarchVoxelGridLongestAxis (Renderer.cuh:760-915) / shadowRayMarchVoxelGridLongestAxis
+    // (:495-631) with performVoxelSpaceJump (:696-751) / performShadowVoxelSpaceJump (:441-492),
+    // as a convergent state machine: every loop iteration makes exactly ONE probe
+    // (existence check, lookup if present) for every lane, whatever it is doing --
+    //   main  : the next axis step of the current iteration of the reference loop
+    //           (M/S in crossing order, then L; g[axis] += ad[axis] first), or
+    //   jump  : performVoxelSpaceJump's `while (!exists(g))` probes (the first one
+    //           re-checks the step's own voxel, as the reference does) and cluster skips,
+    // then advances that lane's state.  Same probes, ticks and bytes, in the same
+    // order, as the nested reference loops; no per-case code copies, no divergent
+    // nesting.  The tail falls back to the original DDA (Renderer.cuh:912).
     template <bool SHADOW>
     __device__ __forceinline__ bool grid_longest(f3& oo, f3 od, uint32_t reg, i3 cr, Hit& h) {
-        LA a;
+        uint32_t L, M, S;
         // Ray::convertRayToLongestAxisDirection (Ray.cuh:19-71)
         float ax = fabsf(od.x), ay = fabsf(od.y), az = fabsf(od.z), k;
         if (ax > ay && ax > az) {
-            a.L = 0; a.M = ay > az ? 1 : 2; a.S = ay > az ? 2 : 1; k = 1.0f / ax;
+            L = 0; M = ay > az ? 1 : 2; S = ay > az ? 2 : 1; k = 1.0f / ax;
         } else if (ay > az) {
-            a.L = 1; a.M = ax > az ? 0 : 2; a.S = ax > az ? 2 : 0; k = 1.0f / ay;
+            L = 1; M = ax > az ? 0 : 2; S = ax > az ? 2 : 0; k = 1.0f / ay;
         } else {
-            a.L = 2; a.M = ax > ay ? 0 : 1; a.S = ax > ay ? 1 : 0; k = 1.0f / az;
+            L = 2; M = ax > ay ? 0 : 1; S = ax > ay ? 1 : 0; k = 1.0f / az;
         }
-        a.ds = scl(k, od);
-        a.old_o = oo;
-        a.g = i3{f2i(oo.x), f2i(oo.y), f2i(oo.z)};
-        a.ad = i3{0, 0, 0};
-        int32_t adL = comp(od, a.L) < 0.0f ? -1 : 1;
-        seti(a.ad, a.L, adL);
-        float gL = (float)geti(a.g, a.L), oL = comp(oo, a.L);
-        float t = adL > 0 ? (gL + kEps + 1.0f - oL) / (float)adL : (gL - kEps - oL) / (float)adL;
-        a.ray_o = add(a.old_o, scl(t, a.ds));
-        seti(a.ad, a.M, f2i(comp(a.ray_o, a.M)) - geti(a.g, a.M));
-        seti(a.ad, a.S, f2i(comp(a.ray_o, a.S)) - geti(a.g, a.S));
-        const bool mid_floor = comp(a.ds, a.M) < 0.0f;   // decimalToIntFunc (:784)
-        bool res = false;
-        while (grid_in_region(geti(a.g, a.L) + geti(a.ad, a.L), geti(a.g, a.M) + geti(a.ad, a.M),
-                              geti(a.g, a.S) + geti(a.ad, a.S))) {
+        const f3 ds = scl(k, od);
+        f3 old_o = oo;
+        i3 g{f2i(oo.x), f2i(oo.y), f2i(oo.z)};
+        i3 ad{0, 0, 0};
+        const int32_t adL = comp(od, L) < 0.0f ? -1 : 1;
+        seti(ad, L, adL);
+        f3 ray_o;
+        {
+            const float gL = (float)geti(g, L), oL = comp(oo, L);
+            const float t = adL > 0 ? (gL + kEps + 1.0f - oL) / (float)adL : (gL - kEps - oL) / (float)adL;
+            ray_o = add(old_o, scl(t, ds));
+        }
+        seti(ad, M, f2i(comp(ray_o, M)) - geti(g, M));
+        seti(ad, S, f2i(comp(ray_o, S)) - geti(g, S));
+        const bool mid_floor = comp(ds, M) < 0.0f;   // decimalToIntFunc (:784)
+        float tX = 0.0f, tY = 0.0f, tZ = 0.0f, tMin = 0.0f;   // the jump's last skip (hit normal)
+        uint32_t seq = 0, rem = 0;                   // pending axis steps of this iteration (2 bits each)
+        bool jumping = false;
+
+        // Top of the reference's `while (isInGrid(grid + diff))` loop: false = loop over
+        // (fall back to the original DDA); aborted = budget exhausted.
+        auto begin_iter = [&]() -> bool {
+            if (!grid_in_region(g.x + ad.x, g.y + ad.y, g.z + ad.z)) return false;
             if (!tick()) return false;
-            int r;
-            int32_t adM = geti(a.ad, a.M), adS = geti(a.ad, a.S);
+            const int32_t adM = geti(ad, M), adS = geti(ad, S);
             if (adS != 0 && adM != 0) {
-                float om = comp(a.old_o, a.M);
-                float t1 = ((mid_floor ? floorf(om) : ceilf(om)) - om) / comp(a.ds, a.M);
-                float sp = comp(a.old_o, a.S) + comp(a.ds, a.S) * t1;
-                int32_t sd = f2i(floorf(sp)) - geti(a.g, a.S);
-                uint32_t a0 = sd != 0 ? a.S : a.M, a1 = sd != 0 ? a.M : a.S;
-                r = axis_step<SHADOW>(oo, a, a0, false, reg, cr, h, res);
-                if (r == 1) return res;
-                if (r == 2) continue;
-                r = axis_step<SHADOW>(oo, a, a1, false, reg, cr, h, res);
-                if (r == 1) return res;
-                if (r == 2) continue;
+                const float om = comp(old_o, M);
+                const float t1 = ((mid_floor ? floorf(om) : ceilf(om)) - om) / comp(ds, M);
+                const float sp = comp(old_o, S) + comp(ds, S) * t1;
+                const int32_t sd = f2i(floorf(sp)) - geti(g, S);
+                const uint32_t a0 = sd != 0 ? S : M, a1 = sd != 0 ? M : S;
+                seq = a0 | (a1 << 2) | (L << 4);
+                rem = 3;
             } else if (adM != 0) {
-                r = axis_step<SHADOW>(oo, a, a.M, false, reg, cr, h, res);
-                if (r == 1) return res;
-                if (r == 2) continue;
+                seq = M | (L << 2);
+                rem = 2;
             } else if (adS != 0) {
-                r = axis_step<SHADOW>(oo, a, a.S, false, reg, cr, h, res);
-                if (r == 1) return res;
-                if (r == 2) continue;
+                seq = S | (L << 2);
+                rem = 2;
+            } else {
+                seq = L;
+                rem = 1;
             }
-            r = axis_step<SHADOW>(oo, a, a.L, true, reg, cr, h, res);
-            if (r == 1) return res;
-            if (r == 2) continue;
-            a.old_o = a.ray_o;
-            a.ray_o = add(a.ray_o, a.ds);
-            seti(a.ad, a.M, f2i(comp(a.ray_o, a.M)) - geti(a.g, a.M));
-            seti(a.ad, a.S, f2i(comp(a.ray_o, a.S)) - geti(a.g, a.S));
+            return true;
+        };
+
+        bool tail = !begin_iter();
+        if (aborted) return false;
+        while (!tail) {
+            const uint32_t axis = seq & 3u;
+            i3 pg = g;
+            if (!jumping) seti(pg, axis, geti(g, axis) + geti(ad, axis));
+            const Blk blk = exists(reg, pg.x, pg.y, pg.z);
+            const bool present = !absent(blk);
+            const uint32_t col = present ? lookup(reg, blk, pg.x, pg.y, pg.z) : kEmpty;
+            g = pg;
+            if (col != kEmpty) {
+                if (!SHADOW) {
+                    h.col = col;
+                    h.region = cr;
+                    h.longest = true;
+                    if (jumping) {                   // performVoxelSpaceJump's hit
+                        h.n = normal_from_t(tX, tY, tZ, tMin, ds);
+                        h.so = old_o;
+                    } else {                         // an axis step's hit
+                        f3 n = mk(0.0f, 0.0f, 0.0f);
+                        setf(n, axis, copysignf(1.0f, -comp(ds, axis)));
+                        h.n = n;
+                        if (axis == L) {
+                            h.so = ray_o;
+                        } else {                     // getLocalHitLocation (Renderer.cuh:753-758)
+                            const float o = comp(old_o, axis), dd = comp(ds, axis);
+                            const float t = dd > 0.0f ? (ceilf(o) - o) / dd : (floorf(o) - o) / dd;
+                            h.so = add(old_o, scl(t, ds));
+                        }
+                    }
+                }
+                return true;
+            }
+            if (!jumping) {
+                if (!present) { jumping = true; continue; }   // performVoxelSpaceJump (re-probes g)
+                seq >>= 2;
+                if (--rem != 0u) continue;
+                old_o = ray_o;                       // end of the iteration (:903-906)
+                ray_o = add(ray_o, ds);
+                seti(ad, M, f2i(comp(ray_o, M)) - geti(g, M));
+                seti(ad, S, f2i(comp(ray_o, S)) - geti(g, S));
+                tail = !begin_iter();
+                if (aborted) return false;
+                continue;
+            }
+            if (!present) {                          // the jump's cluster skip
+                if (!tick()) return false;
+                const int32_t nx = ds.x > 0.0f ? ((g.x / 8) + 1) * 8 : (g.x / 8) * 8;
+                const int32_t ny = ds.y > 0.0f ? ((g.y / 8) + 1) * 8 : (g.y / 8) * 8;
+                const int32_t nz = ds.z > 0.0f ? ((g.z / 8) + 1) * 8 : (g.z / 8) * 8;
+                tX = ((float)nx - old_o.x) / ds.x;
+                tY = ((float)ny - old_o.y) / ds.y;
+                tZ = ((float)nz - old_o.z) / ds.z;
+                tMin = fminf(tX, fminf(tY, tZ)) + kEps;
+                old_o = add(old_o, scl(tMin, ds));
+                g = i3{f2i(floorf(old_o.x)), f2i(floorf(old_o.y)), f2i(floorf(old_o.z))};
+                if (!grid_in_region(g.x, g.y, g.z)) {
+                    oo = old_o;
+                    return false;
+                }
+                continue;
+            }
+            // the jump landed in an existing cluster without a hit: CONTINUE_VAL
+            const float oL = comp(old_o, L), dL = comp(ds, L);
+            const float tNext = dL > 0.0f ? (ceilf(oL) - oL) / dL : (floorf(oL) - oL) / dL;
+            ray_o = add(old_o, scl(tNext + kEps, ds));
+            seti(ad, M, f2i(comp(ray_o, M)) - geti(g, M));
+            seti(ad, S, f2i(comp(ray_o, S)) - geti(g, S));
+            jumping = false;
+            tail = !begin_iter();
+            if (aborted) return false;
         }
-        oo = a.old_o;     // Renderer.cuh:912 (direction of originalRay kept)
+        oo = old_o;     // Renderer.cuh:912 (direction of originalRay kept)
         return grid_original<SHADOW>(oo, od, reg, cr, h);
     }
 

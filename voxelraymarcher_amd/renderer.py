@@ -161,15 +161,21 @@ class VoxelSceneCPU:
     generateVoxelScene = generate_voxel_scene
 
 
-def read_voxel_file(path: str):
-    """VoxelFile::readVoxelFile (VoxelFile.cuh:9-35) -> (xyz int32[n,3], rgb uint32[n])."""
+def _read_scene_file(fn: str, path: str):
     n = c_size_t()
-    check(lib().vr_vox_read(path.encode(), None, None, 0, ctypes.byref(n)), "readVoxelFile")
+    check(getattr(lib(), fn)(path.encode(), None, None, 0, ctypes.byref(n)), fn)
     xyz = np.zeros((max(n.value, 1), 3), dtype=np.int32)
     rgb = np.zeros(max(n.value, 1), dtype=np.uint32)
-    check(lib().vr_vox_read(path.encode(), xyz.ctypes.data_as(ctypes.POINTER(c_int32)),
-                            rgb.ctypes.data_as(ctypes.POINTER(c_uint32)), n.value, ctypes.byref(n)), "readVoxelFile")
+    check(getattr(lib(), fn)(path.encode(), xyz.ctypes.data_as(ctypes.POINTER(c_int32)),
+                             rgb.ctypes.data_as(ctypes.POINTER(c_uint32)), n.value, ctypes.byref(n)), fn)
     return xyz[: n.value].copy(), rgb[: n.value].copy()
+
+
+def read_voxel_file(path: str):
+    """VoxelFile::readVoxelFile (VoxelFile.cuh:9-35) -> (xyz int32[n,3], rgb uint32[n]).
+    Reads the .vox CSV (parsed in parallel, same rules) or, detected by its magic,
+    the .vxb binary sidecar."""
+    return _read_scene_file("vr_scene_file_read", path)
 
 
 def write_voxel_file(path: str, xyz: np.ndarray, rgb: np.ndarray) -> None:
@@ -177,6 +183,14 @@ def write_voxel_file(path: str, xyz: np.ndarray, rgb: np.ndarray) -> None:
     rgb = np.ascontiguousarray(rgb, dtype=np.uint32).reshape(-1)
     check(lib().vr_vox_write(path.encode(), xyz.ctypes.data_as(ctypes.POINTER(c_int32)),
                              rgb.ctypes.data_as(ctypes.POINTER(c_uint32)), rgb.shape[0]), "write_voxel_file")
+
+
+def write_binary_scene(path: str, xyz: np.ndarray, rgb: np.ndarray) -> None:
+    """The .vxb binary sidecar (vr_vxb_write): the same voxels, loaded without parsing."""
+    xyz = np.ascontiguousarray(xyz, dtype=np.int32).reshape(-1, 3)
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint32).reshape(-1)
+    check(lib().vr_vxb_write(path.encode(), xyz.ctypes.data_as(ctypes.POINTER(c_int32)),
+                             rgb.ctypes.data_as(ctypes.POINTER(c_uint32)), rgb.shape[0]), "write_binary_scene")
 
 
 def synth_scene(n: int, p_region: float, p_cluster: float, p_voxel: float, seed: int):
