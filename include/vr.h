@@ -96,6 +96,23 @@ int vr_lighting_default(vr_lighting* out);
 int vr_scene_create(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb,
                     size_t n, vr_scene** out);
 
+/* Where the scene image is built.  DEVICE: region
+ * bucketing, a stable radix sort by (region, cluster, key), last-insertion
+ * dedupe, mask records and cuckoo tables on the GPU; HOST: the same on the
+ * CPU.  Both produce byte-identical device images (vr_scene_digest).  AUTO =
+ * DEVICE (what vr_scene_create uses). */
+typedef enum { VR_BUILD_AUTO = 0, VR_BUILD_DEVICE = 1, VR_BUILD_HOST = 2 } vr_build;
+
+/* vr_scene_create with the voxel arrays optionally already on `device`
+ * (inputs_on_device != 0) and an explicit builder; `stream` orders the device
+ * build (NULL = default stream).  Returns when the scene is ready. */
+int vr_scene_create_ex(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n,
+                       int inputs_on_device, vr_build build, void* stream, vr_scene** out);
+
+/* FNV-1a digest of each device buffer (region table, VCS masks, VCS colours,
+ * cuckoo meta, cuckoo slots) -- to compare builds. */
+int vr_scene_digest(const vr_scene* s, uint64_t out[5]);
+
 /* VoxelFile::readVoxelFile (geometry/VoxelFile.cuh:9-35) + vr_scene_create.
  * Unlike the reference the path is used as given (no "resources/" prefix).
  * Accepts the .vox CSV (parsed in parallel, same rules and first-error line)

@@ -68,6 +68,8 @@ SIGNATURES = {
                                POINTER(VrCamera)]),
     "vr_lighting_default": (c_int, [POINTER(VrLighting)]),
     "vr_scene_create": (c_int, [c_int, c_int, POINTER(c_int32), POINTER(c_uint32), c_size_t, POINTER(c_void_p)]),
+    "vr_scene_create_ex": (c_int, [c_int, c_int, c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, POINTER(c_void_p)]),
+    "vr_scene_digest": (c_int, [c_void_p, POINTER(c_uint64)]),
     "vr_scene_load_vox": (c_int, [c_int, c_int, c_char_p, POINTER(c_void_p)]),
     "vr_scene_get_info": (c_int, [c_void_p, POINTER(VrSceneInfo)]),
     "vr_scene_destroy": (None, [c_void_p]),

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "vr.h"
+#include "vr_build.h"
 #include "vr_internal.h"
 
 namespace {
@@ -181,7 +182,7 @@ struct Rec {
     uint32_t idx;     // insertion order (later wins)
 };
 
-int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, vr_scene** out) {
+int build_scene_host(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, vr_scene** out) {
     if (!out) return fail(VR_E_INVALID, "out is NULL");
     *out = nullptr;
     if (store != VR_STORE_VCS && store != VR_STORE_HASHTABLE) return fail(VR_E_INVALID, "unknown store");
@@ -333,6 +334,72 @@ int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* 
     }
     *out = s;
     return VR_OK;
+}
+
+// Device build (vr_build.hip) from host or device voxel arrays.
+int build_scene_device(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, bool on_device,
+                       hipStream_t stream, vr_scene** out) {
+    DeviceGuard dg(device);
+    const int32_t* dxyz = xyz;
+    const uint32_t* drgb = rgb;
+    void *tx = nullptr, *tc = nullptr;
+    auto release = [&]() {
+        if (tx) (void)hipFree(tx);
+        if (tc) (void)hipFree(tc);
+    };
+    if (!on_device && n) {
+        hipError_t e = hipMalloc(&tx, 3 * n * sizeof(int32_t));
+        if (e == hipSuccess) e = hipMalloc(&tc, n * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemcpyAsync(tx, xyz, 3 * n * sizeof(int32_t), hipMemcpyHostToDevice, stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(tc, rgb, n * sizeof(uint32_t), hipMemcpyHostToDevice, stream);
+        if (e != hipSuccess) { release(); return hip_fail(e, "voxel upload"); }
+        dxyz = (const int32_t*)tx;
+        drgb = (const uint32_t*)tc;
+    }
+    vr::GpuScene g;
+    std::string err;
+    const int rc = vr::build_scene_gpu((int)store, dxyz, drgb, n, stream, g, err);
+    release();
+    vr_scene* s = new vr_scene();
+    s->device = device; s->store = store; s->D = g.D; s->min_coord = g.min_coord;
+    s->n_regions = g.n_regions; s->n_voxels = g.n_voxels;
+    s->region_slot = DevBuf{g.region_slot, g.region_slot_bytes};
+    s->vcs_mask = DevBuf{g.vcs_mask, g.vcs_mask_bytes};
+    s->vcs_vals = DevBuf{g.vcs_vals, g.vcs_vals_bytes};
+    s->ht_meta = DevBuf{g.ht_meta, g.ht_meta_bytes};
+    s->ht_slots = DevBuf{g.ht_slots, g.ht_slots_bytes};
+    if (rc) {
+        free_scene(s);
+        return fail(rc == -1 ? VR_E_INVALID : rc == -5 ? VR_E_BUILD : VR_E_HIP, "scene build: " + err);
+    }
+    *out = s;
+    return VR_OK;
+}
+
+int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, bool on_device,
+                vr_build mode, void* stream, vr_scene** out) {
+    if (!out) return fail(VR_E_INVALID, "out is NULL");
+    *out = nullptr;
+    if (store != VR_STORE_VCS && store != VR_STORE_HASHTABLE) return fail(VR_E_INVALID, "unknown store");
+    if (n && (!xyz || !rgb)) return fail(VR_E_INVALID, "xyz/rgb NULL");
+    if (n >= 0xFFFFFFFFull) return fail(VR_E_INVALID, "too many voxels");
+    if (mode != VR_BUILD_AUTO && mode != VR_BUILD_DEVICE && mode != VR_BUILD_HOST) return fail(VR_E_INVALID, "unknown build mode");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(VR_E_HIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(VR_E_INVALID, "device index out of range");
+    if (mode == VR_BUILD_HOST) {
+        if (!on_device) return build_scene_host(device, store, xyz, rgb, n, out);
+        DeviceGuard dg(device);
+        std::vector<int32_t> hx(3 * n + 3);
+        std::vector<uint32_t> hc(n + 1);
+        if (n) {
+            hipError_t e = hipMemcpy(hx.data(), xyz, 3 * n * sizeof(int32_t), hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(hc.data(), rgb, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return hip_fail(e, "voxel download");
+        }
+        return build_scene_host(device, store, hx.data(), hc.data(), n, out);
+    }
+    return build_scene_device(device, store, xyz, rgb, n, on_device, (hipStream_t)stream, out);
 }
 
 vr::KScene kscene(const vr_scene* s) {
@@ -657,7 +724,29 @@ int vr_lighting_default(vr_lighting* out) {
 }
 
 int vr_scene_create(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, vr_scene** out) {
-    return build_scene(device, store, xyz, rgb, n, out);
+    return build_scene(device, store, xyz, rgb, n, false, VR_BUILD_AUTO, nullptr, out);
+}
+
+int vr_scene_create_ex(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, int inputs_on_device,
+                       vr_build build, void* stream, vr_scene** out) {
+    return build_scene(device, store, xyz, rgb, n, inputs_on_device != 0, build, stream, out);
+}
+
+int vr_scene_digest(const vr_scene* s, uint64_t out[5]) {
+    if (!s || !out) return fail(VR_E_INVALID, "NULL argument");
+    DeviceGuard dg(s->device);
+    const DevBuf* bufs[5] = {&s->region_slot, &s->vcs_mask, &s->vcs_vals, &s->ht_meta, &s->ht_slots};
+    for (int i = 0; i < 5; ++i) {
+        uint64_t h = 1469598103934665603ull ^ bufs[i]->bytes;     // FNV-1a over the buffer bytes
+        if (bufs[i]->p && bufs[i]->bytes) {
+            std::vector<unsigned char> host(bufs[i]->bytes);
+            hipError_t e = hipMemcpy(host.data(), bufs[i]->p, bufs[i]->bytes, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return hip_fail(e, "hipMemcpy D2H");
+            for (unsigned char c : host) h = (h ^ c) * 1099511628211ull;
+        }
+        out[i] = h;
+    }
+    return VR_OK;
 }
 
 int vr_scene_load_vox(int device, vr_store store, const char* path, vr_scene** out) {
@@ -670,7 +759,7 @@ int vr_scene_load_vox(int device, vr_store store, const char* path, vr_scene** o
         std::vector<uint32_t> rgb(n + 1);
         rc = vr_vxb_read(path, xyz.data(), rgb.data(), n, &n);
         if (rc) return rc;
-        return build_scene(device, store, xyz.data(), rgb.data(), n, out);
+        return build_scene(device, store, xyz.data(), rgb.data(), n, false, VR_BUILD_AUTO, nullptr, out);
     }
     std::vector<char> text;                 // CSV: read and parse once
     int rc = read_file(path, text);
@@ -679,7 +768,7 @@ int vr_scene_load_vox(int device, vr_store store, const char* path, vr_scene** o
     rc = parse_vox_text(path, text, vp);
     if (rc) return rc;
     std::vector<char>().swap(text);
-    return build_scene(device, store, vp.xyz.data(), vp.rgb.data(), vp.rgb.size(), out);
+    return build_scene(device, store, vp.xyz.data(), vp.rgb.data(), vp.rgb.size(), false, VR_BUILD_AUTO, nullptr, out);
 }
 
 int vr_scene_get_info(const vr_scene* s, vr_scene_info* out) {

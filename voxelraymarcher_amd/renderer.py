@@ -103,6 +103,12 @@ class DeviceScene:
                 "store": StorageType(i.store), "voxel_count": i.voxel_count, "device_bytes": i.device_bytes,
                 "device": i.device}
 
+    def digest(self) -> tuple:
+        """FNV-1a of (region table, VCS masks, VCS colours, cuckoo meta, cuckoo slots)."""
+        d = (ctypes.c_uint64 * 5)()
+        check(lib().vr_scene_digest(self.handle, d), "vr_scene_digest")
+        return tuple(int(x) for x in d)
+
     def close(self) -> None:
         if self._h:
             lib().vr_scene_destroy(self._h)
@@ -121,15 +127,38 @@ class DeviceScene:
         self.close()
 
 
-def create_scene(xyz: np.ndarray, rgb: np.ndarray, store: StorageType, device: int = 0) -> DeviceScene:
-    """generateVoxelScene(storageType) over the voxels (VoxelSceneCPU.cuh:49-93)."""
+class Build(enum.IntEnum):
+    """vr_build: where the scene image is built (both give identical images)."""
+    AUTO = 0
+    DEVICE = 1
+    HOST = 2
+
+
+def _build_stream(stream) -> c_void_p:
+    return c_void_p(None) if stream is None else c_void_p(stream.cuda_stream)
+
+
+def create_scene(xyz, rgb, store: StorageType, device: int = 0, build: Build = Build.AUTO, stream=None) -> DeviceScene:
+    """generateVoxelScene(storageType) over the voxels (VoxelSceneCPU.cuh:49-93).
+    xyz/rgb: numpy arrays, or torch tensors already on the GPU (int32 [n,3] / [n])."""
+    h = c_void_p()
+    if hasattr(xyz, "is_cuda") and xyz.is_cuda:
+        import torch
+        xyz = xyz.to(torch.int32).contiguous().reshape(-1, 3)
+        rgb = rgb.to(torch.int32).contiguous().reshape(-1)
+        if xyz.shape[0] != rgb.shape[0]:
+            raise ValueError("xyz and rgb lengths differ")
+        check(lib().vr_scene_create_ex(int(device), int(store), c_void_p(xyz.data_ptr()), c_void_p(rgb.data_ptr()),
+                                       rgb.shape[0], 1, int(build), _build_stream(stream), ctypes.byref(h)),
+              "generateVoxelScene")
+        return DeviceScene(h)
     xyz = np.ascontiguousarray(xyz, dtype=np.int32).reshape(-1, 3)
     rgb = np.ascontiguousarray(rgb, dtype=np.uint32).reshape(-1)
     if xyz.shape[0] != rgb.shape[0]:
         raise ValueError("xyz and rgb lengths differ")
-    h = c_void_p()
-    check(lib().vr_scene_create(int(device), int(store), xyz.ctypes.data_as(ctypes.POINTER(c_int32)),
-                                rgb.ctypes.data_as(ctypes.POINTER(c_uint32)), rgb.shape[0], ctypes.byref(h)),
+    check(lib().vr_scene_create_ex(int(device), int(store), xyz.ctypes.data_as(ctypes.c_void_p),
+                                   rgb.ctypes.data_as(ctypes.c_void_p), rgb.shape[0], 0, int(build),
+                                   _build_stream(stream), ctypes.byref(h)),
           "generateVoxelScene")
     return DeviceScene(h)
 
