@@ -420,7 +420,6 @@ int make_view(const vr_scene* s, const vr_camera* cam, const vr_lighting* lit, c
     if (!cam || !lit) return fail(VR_E_INVALID, "camera/lighting NULL");
     if (width == 0 || height == 0 || width > 65536 || height > 65536) return fail(VR_E_INVALID, "bad image size");
     memset(&v, 0, sizeof v);
-    if (const char* e = getenv("VR_EXPERIMENT")) v.experiment = (uint32_t)atoi(e);
     for (int i = 0; i < 3; ++i) {
         v.llc[i] = cam->lower_left[i]; v.hor[i] = cam->horizontal[i]; v.ver[i] = cam->vertical[i];
         v.org[i] = cam->origin[i];

@@ -54,7 +54,6 @@ struct KView {
     unsigned long long* bytes;
     uint32_t* defer;          // crawl deferral slot: [count, done, entries (l << 16 | x)...]
     uint32_t defer_cap;
-    uint32_t experiment;      // VR_EXPERIMENT (tuning A/B only; 0 in production)
 };
 
 // Rays that start a cluster-skip crawl (see vr_march.hip crawl_steps) in the
