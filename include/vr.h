@@ -87,6 +87,12 @@ int vr_camera_make(const float eye[3], const float look_at[3], const float up[3]
  * normalize(1,1,1), white, point light at (10,10,-10) disabled, shadows on. */
 int vr_lighting_default(vr_lighting* out);
 
+/* Light direction as the reference uploads it: makeUnitVector(dir)
+ * (Main.cu:28, Vector3.cuh:162-165: v / sqrtf(x*x+y*y+z*z), three divides).
+ * VR_E_INVALID for a zero, NaN or infinite vector. Other lighting fields are
+ * plain data (light_color, light_pos, use_point_light, use_shadows). */
+int vr_lighting_set_direction(vr_lighting* lit, const float dir[3]);
+
 /* VoxelSceneCPU::insertVoxel for every voxel (VoxelSceneCPU.cuh:16-46), then
  * generateVoxelScene(storageType) (:49-93) -- VoxelClusterStore ctor
  * (storage/VoxelClusterStore.cuh:37-85) or CuckooHashTable ctor
@@ -180,6 +186,19 @@ int vr_render_count(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
 /* writeColorToFramebuffer (Renderer.cuh:1024-1031): packed words -> RGB8
  * (3 bytes per pixel, R = word >> 16 truncated to 8 bits), on the device. */
 int vr_pack_rgb8(const uint32_t* words_dev, uint8_t* rgb_dev, uint64_t n_pixels, void* stream);
+
+/* ImageWriter::writeImage(filename, image, width, height, colorChannels)
+ * (ImageWriter.cpp:8-16, stbi_write_png with tightly packed rows): 8-bit PNG
+ * of 1-4 channels from HOST memory. Row chunks are deflated on parallel
+ * threads (level 0-9, out-of-range = 6). Pixels are what stb would store; the
+ * compressed bytes differ. */
+int vr_png_write(const char* path, const uint8_t* image, uint32_t width, uint32_t height, int channels, int level);
+
+/* Same encoder into memory. out == NULL: sets *out_len to an upper bound of
+ * the encoded size (no encoding); otherwise encodes and sets the actual size.
+ * threads <= 0: hardware threads, at most 16. */
+int vr_png_encode(const uint8_t* image, uint32_t width, uint32_t height, int channels, int level, int threads,
+                  uint8_t* out, size_t capacity, size_t* out_len);
 
 /* Synthetic scene: with xyz == NULL only counts (*n_out); otherwise writes up
  * to `capacity` voxels (3 int32 + 1 colour each) and sets *n_out. */

@@ -127,6 +127,12 @@ inline vr_lighting defaultLighting() {
     return l;
 }
 
+// LIGHT_DIRECTION = makeUnitVector(dir) (Main.cu:28).
+inline void setLightDirection(vr_lighting& l, float x, float y, float z) {
+    const float d[3] = {x, y, z};
+    check(vr_lighting_set_direction(&l, d), "setLightDirection");
+}
+
 // Launch on `stream` (hipStream_t as void*); asynchronous.
 inline void runRaymarchingKernel(uint32_t width, uint32_t height, RayMarchAlgorithm algo, const Camera& camera,
                                  const VoxelSceneInfo& info, const DeviceScene& scene, const vr_lighting& lighting,

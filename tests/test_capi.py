@@ -68,6 +68,22 @@ def test_lighting_defaults():
     assert bytes(lit) == bytes(o)
 
 
+@pytest.mark.parametrize("d", [(1.0, 1.0, 1.0), (0.0, 1.0, 0.0), (-1.0, 2.0, -0.5), (3e-20, 1e-20, -2e-20)])
+def test_light_direction_is_make_unit_vector(d):
+    """Main.cu:28 makeUnitVector = v / sqrtf(x*x+y*y+z*z) in fp32 (Vector3.cuh:79,162-165)."""
+    f = np.float32
+    x, y, z = (f(c) for c in d)
+    ln = np.sqrt(f(f(f(x * x) + f(y * y)) + f(z * z)), dtype=np.float32)
+    want = [f(x / ln), f(y / ln), f(z / ln)]
+    lit = vr.setup_constant_values(light_direction=d, light_color=(0.5, 1.0, 2.0))
+    assert [f(v) for v in lit.light_dir] == want
+    assert list(lit.light_color) == [0.5, 1.0, 2.0]
+    if d == (1.0, 1.0, 1.0):
+        assert list(lit.light_dir) == list(oracle.lighting().light_dir)
+    with pytest.raises(vr.VrError):
+        vr.setup_constant_values(light_direction=(0.0, 0.0, 0.0))
+
+
 @pytest.mark.parametrize("name", ["C1", "C2", "C5"])
 def test_synth_generator_matches_numpy(name):
     cfg = vr.CONFIGS[name]
@@ -139,6 +155,10 @@ def test_cli_binary_built():
     assert os.access(exe, os.X_OK)
     out = os.popen(f"{exe} --help").read()
     assert "hashtable|vcs" in out
+    for flag in ("--no-shadows", "--point-light", "--light-dir", "--light-color"):
+        assert flag in out
+    r = os.popen(f"{exe} --light-dir 1,2 2>&1; echo rc=$?").read()
+    assert "needs X,Y,Z" in r and "rc=2" in r
 
 
 def test_cli_converts_scene_to_vxb(tmp_path):

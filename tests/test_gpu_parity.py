@@ -175,6 +175,24 @@ def test_lighting_variants(c1, store, algo):
         check_frame(*c1, store, algo, 96, 96, cfg.scale, lit=lit)
 
 
+LIGHTS = [((0.0, 1.0, 0.0), (1.0, 1.0, 1.0)),        # two zero components: guarded shadow divisions
+          ((1.0, 1.0, 0.0), (0.5, 1.0, 0.25)),       # long-axis tie x = y (strict '>' picks y)
+          ((-1.0, 2.0, -0.5), (1.0, 0.75, 2.0)),     # negative steps, channel overflow clamps by truncation
+          ((0.0, -1.0, 1.0), (1.0, 1.0, 1.0))]
+
+
+@pytest.mark.parametrize("store", STORES, ids=lambda s: s.name)
+@pytest.mark.parametrize("algo", ALGOS, ids=lambda a: a.name)
+def test_light_direction_and_color(c1, c2, store, algo):
+    """the setupConstantValues block as parameters -- light
+    direction (through makeUnitVector) and colour change shading and the shadow walk."""
+    for i, (d, col) in enumerate(LIGHTS):
+        lit = vr.setup_constant_values(light_direction=d, light_color=col)
+        check_frame(*c1, store, algo, 96, 96, vr.CONFIGS["C1"].scale, lit=lit)
+        if i < 2:
+            check_frame(*c2, store, algo, 240, 136, vr.CONFIGS["C2"].scale, lit=lit, kernels=[vr.Kernel.TILE])
+
+
 @pytest.mark.parametrize("algo", ALGOS, ids=lambda a: a.name)
 def test_camera_inside_grid_and_translation(c1, algo):
     cam = vr.Camera((2.0, 2.5, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 90.0, 1.5)

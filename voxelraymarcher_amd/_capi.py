@@ -67,6 +67,9 @@ SIGNATURES = {
     "vr_camera_make": (c_int, [POINTER(c_float), POINTER(c_float), POINTER(c_float), c_float, c_float,
                                POINTER(VrCamera)]),
     "vr_lighting_default": (c_int, [POINTER(VrLighting)]),
+    "vr_lighting_set_direction": (c_int, [POINTER(VrLighting), POINTER(c_float)]),
+    "vr_png_write": (c_int, [c_char_p, c_void_p, c_uint32, c_uint32, c_int, c_int]),
+    "vr_png_encode": (c_int, [c_void_p, c_uint32, c_uint32, c_int, c_int, c_int, c_void_p, c_size_t, POINTER(c_size_t)]),
     "vr_scene_create": (c_int, [c_int, c_int, POINTER(c_int32), POINTER(c_uint32), c_size_t, POINTER(c_void_p)]),
     "vr_scene_create_ex": (c_int, [c_int, c_int, c_void_p, c_void_p, c_size_t, c_int, c_int, c_void_p, POINTER(c_void_p)]),
     "vr_scene_digest": (c_int, [c_void_p, POINTER(c_uint64)]),

@@ -4,13 +4,14 @@
 //                   [--scene resources/scene.vox] [--width 1920] [--height 1080]
 //                   [--out output.png] [--device 0] [--synth N] [--repeat K]
 //                   [--write-vxb F]   (convert the scene to the .vxb sidecar and exit)
+//                   [--no-shadows] [--point-light X,Y,Z] [--light-dir X,Y,Z] [--light-color R,G,B]
+//                   (the setupConstantValues toggles, Main.cu:26-42, as flags)
 // Defaults follow Main.cu: VCS unless "hashtable", longest axis unless
 // "original" (:45-68), 1920x1080 (:195-196), camera (6,2,6)->(0,0,-1) fov 60
 // (:199), translation 0 (:215), scene file resources/scene.vox (:96-103).
 // The kernel time is measured with HIP events (the reference: std::chrono
 // around launch + sync, :114,160-162).
 #include <hip/hip_runtime.h>
-#include <zlib.h>
 
 #include <chrono>
 #include <cstdio>
@@ -24,6 +25,21 @@
 
 namespace {
 
+// "x,y,z" -> 3 floats; false on malformed input.
+bool parse_vec3(const char* s, float out[3]) {
+    char* end = nullptr;
+    for (int i = 0; i < 3; ++i) {
+        out[i] = std::strtof(s, &end);
+        if (end == s) return false;
+        s = end;
+        if (i < 2) {
+            if (*s != ',') return false;
+            ++s;
+        }
+    }
+    return *s == 0;
+}
+
 bool is_integer(const char* s) {
     if (!s || !*s) return false;
     if (*s == '-' || *s == '+') ++s;
@@ -31,46 +47,6 @@ bool is_integer(const char* s) {
     for (; *s; ++s)
         if (*s < '0' || *s > '9') return false;
     return true;
-}
-
-void put32(std::vector<unsigned char>& v, uint32_t x) {
-    v.push_back((unsigned char)(x >> 24)); v.push_back((unsigned char)(x >> 16));
-    v.push_back((unsigned char)(x >> 8)); v.push_back((unsigned char)x);
-}
-
-void chunk(FILE* f, const char* type, const std::vector<unsigned char>& data) {
-    std::vector<unsigned char> buf;
-    put32(buf, (uint32_t)data.size());
-    buf.insert(buf.end(), type, type + 4);
-    buf.insert(buf.end(), data.begin(), data.end());
-    uLong crc = crc32(0L, Z_NULL, 0);
-    crc = crc32(crc, buf.data() + 4, (uInt)(buf.size() - 4));
-    put32(buf, (uint32_t)crc);
-    fwrite(buf.data(), 1, buf.size(), f);
-}
-
-// ImageWriter::writeImage -> stbi_write_png (ImageWriter.cpp:8-16): 8-bit RGB PNG.
-bool write_png(const char* path, const uint8_t* rgb, uint32_t w, uint32_t h) {
-    std::vector<unsigned char> raw((size_t)(3 * w + 1) * h);
-    for (uint32_t y = 0; y < h; ++y) {
-        raw[(size_t)y * (3 * w + 1)] = 0;
-        std::memcpy(&raw[(size_t)y * (3 * w + 1) + 1], rgb + (size_t)y * 3 * w, 3 * (size_t)w);
-    }
-    uLongf zlen = compressBound((uLong)raw.size());
-    std::vector<unsigned char> z(zlen);
-    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 6) != Z_OK) return false;
-    z.resize(zlen);
-    FILE* f = std::fopen(path, "wb");
-    if (!f) return false;
-    const unsigned char sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
-    fwrite(sig, 1, 8, f);
-    std::vector<unsigned char> ihdr;
-    put32(ihdr, w); put32(ihdr, h);
-    ihdr.push_back(8); ihdr.push_back(2); ihdr.push_back(0); ihdr.push_back(0); ihdr.push_back(0);
-    chunk(f, "IHDR", ihdr);
-    chunk(f, "IDAT", z);
-    chunk(f, "IEND", {});
-    return std::fclose(f) == 0;
 }
 
 #define HIP_OK(x)                                                                        \
@@ -89,6 +65,11 @@ int main(int argc, char* argv[]) {
     std::string scene_path = "resources/scene.vox", out_path = "output.png", vxb_path;
     uint32_t width = 1920, height = 1080, synth = 0;
     int device = 0, repeat = 1;
+    bool shadows = true, point_light = false, has_dir = false;
+    float light_pos[3] = {10.0f, 10.0f, -10.0f}, light_dir[3] = {1.0f, 1.0f, 1.0f}, light_color[3] = {1.0f, 1.0f, 1.0f};
+    auto vec3 = [](const char* name, const char* v, float out[3]) {
+        if (!parse_vec3(v, out)) { std::cerr << name << " needs X,Y,Z" << std::endl; std::exit(2); }
+    };
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto next = [&](const char* name) -> const char* {
@@ -103,9 +84,14 @@ int main(int argc, char* argv[]) {
         else if (a == "--synth") synth = (uint32_t)std::strtoul(next("--synth"), nullptr, 10);
         else if (a == "--repeat") repeat = std::max(1, std::atoi(next("--repeat")));
         else if (a == "--write-vxb") vxb_path = next("--write-vxb");
+        else if (a == "--no-shadows") shadows = false;
+        else if (a == "--point-light") { point_light = true; vec3("--point-light", next("--point-light"), light_pos); }
+        else if (a == "--light-dir") { has_dir = true; vec3("--light-dir", next("--light-dir"), light_dir); }
+        else if (a == "--light-color") vec3("--light-color", next("--light-color"), light_color);
         else if (a == "-h" || a == "--help") {
             std::cout << "usage: VoxelRaymarcher [scale] {hashtable|vcs} {original|longestaxis} [--scene F] "
-                         "[--width W] [--height H] [--out F] [--device N] [--synth N] [--repeat K] [--write-vxb F]" << std::endl;
+                         "[--width W] [--height H] [--out F] [--device N] [--synth N] [--repeat K] [--write-vxb F] "
+                         "[--no-shadows] [--point-light X,Y,Z] [--light-dir X,Y,Z] [--light-color R,G,B]" << std::endl;
             return 0;
         } else pos.push_back(argv[i]);
     }
@@ -173,6 +159,13 @@ int main(int argc, char* argv[]) {
         vrx::Camera camera({6.0f, 2.0f, 6.0f}, {0.0f, 0.0f, -1.0f}, {0.0f, 1.0f, 0.0f}, 60.0f, aspect);
         vrx::VoxelSceneInfo sinfo({0.0f, 0.0f, 0.0f}, scale);
         vr_lighting lit = vrx::defaultLighting();
+        if (has_dir) vrx::setLightDirection(lit, light_dir[0], light_dir[1], light_dir[2]);
+        for (int i = 0; i < 3; ++i) {
+            lit.light_color[i] = light_color[i];
+            lit.light_pos[i] = light_pos[i];
+        }
+        lit.use_point_light = point_light;                       // Main.cu:37
+        lit.use_shadows = shadows;                               // Main.cu:40
 
         uint32_t* fb = nullptr;
         uint8_t* rgb = nullptr;
@@ -194,16 +187,28 @@ int main(int argc, char* argv[]) {
         std::cout << hipGetErrorString(hipGetLastError()) << std::endl;
         std::cout << "Execution Time for Ray Marching Algorithm is: " << (long long)(best_ms * 1000.0f)
                   << " microseconds (" << (double)width * height / (best_ms * 1e3) << " Mrays/s)" << std::endl;
+        // writeResultingImageToDisk (Main.cu:165-174): RGB8 pack on the device,
+        // async copy into pinned memory, parallel PNG encode (vr_png_write).
+        const size_t nbytes = (size_t)width * height * 3;
+        uint8_t* host = nullptr;
+        HIP_OK(hipHostMalloc((void**)&host, nbytes, hipHostMallocDefault));
+        auto t0 = std::chrono::steady_clock::now();
         vrx::check(vr_pack_rgb8(fb, rgb, (uint64_t)width * height, nullptr), "pack");
-        std::vector<uint8_t> host((size_t)width * height * 3);
-        HIP_OK(hipMemcpy(host.data(), rgb, host.size(), hipMemcpyDeviceToHost));
-        if (!write_png(out_path.c_str(), host.data(), width, height)) {
-            std::cerr << "cannot write " << out_path << std::endl;
-            return 1;
-        }
-        std::cout << "Wrote " << out_path << std::endl;
+        HIP_OK(hipMemcpyAsync(host, rgb, nbytes, hipMemcpyDeviceToHost, nullptr));
+        HIP_OK(hipStreamSynchronize(nullptr));
+        auto t1 = std::chrono::steady_clock::now();
+        int rc = vr_png_write(out_path.c_str(), host, width, height, 3, 6);
+        auto t2 = std::chrono::steady_clock::now();
+        (void)hipHostFree(host);
         (void)hipFree(fb);
         (void)hipFree(rgb);
+        if (rc != VR_OK) {
+            std::cerr << "ERROR: Failed to write image to: " << out_path << " (" << vr_last_error() << ")" << std::endl;
+            return 1;
+        }
+        std::cout << "Wrote " << out_path << " (pack+copy "
+                  << std::chrono::duration<double, std::milli>(t1 - t0).count() << " ms, png "
+                  << std::chrono::duration<double, std::milli>(t2 - t1).count() << " ms)" << std::endl;
     } catch (const vrx::Error& e) {
         std::cerr << e.what() << std::endl;
         return 1;

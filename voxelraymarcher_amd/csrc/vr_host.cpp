@@ -688,6 +688,10 @@ bool is_vxb(const char* path) {
 
 }  // namespace
 
+namespace vr {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace vr
+
 extern "C" {
 
 const char* vr_last_error(void) { return g_err.c_str(); }
@@ -719,6 +723,15 @@ int vr_lighting_default(vr_lighting* out) {
     out->light_pos[0] = 10.0f; out->light_pos[1] = 10.0f; out->light_pos[2] = -10.0f;   // :34
     out->use_point_light = 0;                                   // :37
     out->use_shadows = 1;                                       // :40
+    return VR_OK;
+}
+
+int vr_lighting_set_direction(vr_lighting* lit, const float dir[3]) {
+    if (!lit || !dir) return fail(VR_E_INVALID, "NULL argument");
+    f3 L = unit(f3{dir[0], dir[1], dir[2]});                     // Main.cu:28 makeUnitVector
+    if (!std::isfinite(L.x) || !std::isfinite(L.y) || !std::isfinite(L.z))
+        return fail(VR_E_INVALID, "light direction must be a finite non-zero vector");
+    lit->light_dir[0] = L.x; lit->light_dir[1] = L.y; lit->light_dir[2] = L.z;
     return VR_OK;
 }
 

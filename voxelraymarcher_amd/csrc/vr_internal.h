@@ -5,7 +5,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace vr {
+
+// Sets the thread's vr_last_error() message and returns `code` (vr_host.cpp).
+int set_error(int code, const std::string& msg);
 
 constexpr uint32_t kEmpty = 1u << 30;        // EMPTY_KEY == EMPTY_VAL (VoxelFunctions.cuh:20-21)
 constexpr uint32_t kNone = 0xFFFFFFFFu;      // null region / null cluster in the tables

@@ -66,14 +66,21 @@ class Camera:
 
 
 def setup_constant_values(use_shadows: bool = True, use_point_light: bool = False,
-                          light_position=(10.0, 10.0, -10.0)) -> _capi.VrLighting:
-    """setupConstantValues (Main.cu:26-42) -> the lighting block."""
+                          light_position=(10.0, 10.0, -10.0), light_direction=None,
+                          light_color=(1.0, 1.0, 1.0)) -> _capi.VrLighting:
+    """setupConstantValues (Main.cu:26-42) -> the lighting block. The defaults are
+    the reference's; `light_direction` (un-normalised, default (1,1,1)) goes through
+    makeUnitVector exactly as Main.cu:28 does it."""
     lit = _capi.VrLighting()
     check(lib().vr_lighting_default(ctypes.byref(lit)), "setupConstantValues")
+    if light_direction is not None:
+        d = (ctypes.c_float * 3)(*[float(c) for c in light_direction])
+        check(lib().vr_lighting_set_direction(ctypes.byref(lit), d), "light direction")
     lit.use_shadows = int(bool(use_shadows))
     lit.use_point_light = int(bool(use_point_light))
     for i in range(3):
         lit.light_pos[i] = float(light_position[i])
+        lit.light_color[i] = float(light_color[i])
     return lit
 
 
