@@ -49,26 +49,36 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(cfg, xyz, rgb, threads: int) -> dict:
-    """Oracle (clean-room C restatement, OpenMP) on the host cores over the
-    same workload: whole frames of the config, repeated until about 16 s of
-    CPU time (threads x wall) has been spent, after one untimed frame."""
-    import oracle
-    scene = oracle.Scene(xyz, rgb, int(cfg.store))
-    cam = oracle.reference_camera(cfg.width, cfg.height)
-    lit = oracle.lighting()
+def _oracle_rate(scene, cam, lit, cfg, threads: int, cpu_seconds: float):
+    """Whole frames of the config, repeated until about `cpu_seconds` of CPU
+    time (threads x wall) has been spent, after one untimed frame."""
     t0 = time.perf_counter()
     scene.render(int(cfg.algorithm), cam, lit, cfg.width, cfg.height, cfg.scale, nthreads=threads)
     first = time.perf_counter() - t0
-    reps = int(min(60, max(1, np.ceil(16.0 / max(first * threads, 1e-3)))))
+    reps = int(min(60, max(1, np.ceil(cpu_seconds / max(first * threads, 1e-3)))))
     t0 = time.perf_counter()
     for _ in range(reps):
         scene.render(int(cfg.algorithm), cam, lit, cfg.width, cfg.height, cfg.scale, nthreads=threads)
     dt = time.perf_counter() - t0
+    return reps, dt, cfg.width * cfg.height * reps / dt / 1e6
+
+
+def cpu_baseline(cfg, xyz, rgb, threads: int) -> dict:
+    """Oracle (clean-room C restatement, OpenMP dynamic over 8x8 tiles) on the
+    host cores over the same workload: on `threads` cores (~16
+    CPU-s) and on one core (~4 s)."""
+    import oracle
+    scene = oracle.Scene(xyz, rgb, int(cfg.store))
+    cam = oracle.reference_camera(cfg.width, cfg.height)
+    lit = oracle.lighting()
+    reps, dt, rate = _oracle_rate(scene, cam, lit, cfg, threads, 16.0)
+    reps1, dt1, rate1 = _oracle_rate(scene, cam, lit, cfg, 1, 4.0)
     rays = cfg.width * cfg.height * reps
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+    return {"value": round(rate, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{reps} full {cfg.width}x{cfg.height} frames of {cfg.name} ({rays} primary rays, "
-                      f"{dt * threads:.1f} CPU-s), oracle/vr_oracle.c -O2 OpenMP {threads} threads, {dt:.2f} s wall"}
+                      f"{dt * threads:.1f} CPU-s), oracle/vr_oracle.c -O2 OpenMP {threads} threads, {dt:.2f} s wall",
+            "single_core": {"value": round(rate1, 3), "unit": "Mrays/s", "cores": 1,
+                            "sample": f"{reps1} full frames, {dt1:.2f} s"}}
 
 
 def main():
@@ -97,13 +107,16 @@ def main():
     def render(buf):
         vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, rank, world, buf, stream)
 
-    # algorithmic bytes of the frame (instrumented kernel, untimed)
+    # algorithmic bytes of THIS rank's launch (its bands; instrumented kernel,
+    # untimed) and of the whole frame (sum over ranks)
     ctr = torch.zeros(1, dtype=torch.int64, device=dev)
-    full = torch.empty(W * H, dtype=torch.int32, device=dev)
-    vr.render_count(scene, cfg.algorithm, cam, lit, info, W, H, full, ctr)
+    vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, pipe.bufs[0], band_rows=BAND_ROWS, rank=rank,
+                 nranks=world, counter=ctr)
     torch.cuda.synchronize()
+    launch_bytes = int(ctr.item())
+    if world > 1:
+        dist.all_reduce(ctr)
     frame_bytes = int(ctr.item())
-    del full
 
     for _ in range(args.warmup):
         pipe.step(render)
@@ -117,7 +130,24 @@ def main():
         render(pipe.bufs[0])
         b.record(stream)
     torch.cuda.synchronize()
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_all = [a.elapsed_time(b) for a, b in ev]
+    kern_ms = float(np.mean(kern_all))
+    kern_median = float(np.median(kern_all))
+
+    # N > 1: latency of ONE frame, first launch -> gathered and assembled on
+    # rank 0, without the overlap of the pipelined loop
+    frame_latency_ms = None
+    if world > 1:
+        lat = []
+        for _ in range(5):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pipe.step(render)
+            pipe.drain()
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t0)
+        frame_latency_ms = float(np.median(lat)) * 1e3
 
     if world > 1:
         dist.barrier()
@@ -138,8 +168,6 @@ def main():
     mrays = W * H / (ms_per_step * 1e-3) / 1e6
 
     if rank == 0:
-        # bytes of this rank's launch ~ frame bytes / world (bands interleave finely)
-        launch_bytes = frame_bytes / world
         achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
         try:
@@ -169,11 +197,14 @@ def main():
                        "voxels": int(len(rgb)), "parallelism": f"row-band tiles x{world}" +
                        (" + RCCL gather to rank 0 (overlapped with the next frame)" if world > 1 else "")},
             "kernel_ms": round(kern_ms, 4),
+            "kernel_ms_median": round(kern_median, 4),
             "kernel_mrays_per_s": round(W * H / world / (kern_ms * 1e-3) / 1e6, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": int(launch_bytes)},
+                         "algorithmic_bytes_per_launch": launch_bytes, "algorithmic_bytes_per_frame": frame_bytes},
         }
+        if frame_latency_ms is not None:
+            line["frame_latency_ms"] = round(frame_latency_ms, 4)
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(cfg, xyz, rgb, threads)
