@@ -94,6 +94,11 @@ __device__ __forceinline__ float div_fast(float n, const Rcp& c) {
 __device__ __forceinline__ float next_plane(float o, float s, float eps) {
     return s * (ceilf(s * o) + eps);
 }
+// The same as one fma with se = s * EPSILON (exact): s * ceilf(s * o) is exact,
+// so fma rounds s * c + s * eps once, = s * RN(c + eps) by the same symmetry.
+__device__ __forceinline__ float next_plane_fma(float o, float s, float se) {
+    return __builtin_fmaf(s, ceilf(s * o), se);
+}
 
 // CuckooHashTable::hashFunc1 / hashFunc2 (CuckooHashTable.cuh:181-202),
 // int arithmetic with arithmetic right shifts.
@@ -192,7 +197,17 @@ struct Ctx {
         return s.vcs_mask + (size_t)reg * 8192u + (slot << 4);
     }
     __device__ __forceinline__ static uint32_t word_index(uint32_t x, uint32_t y, uint32_t z) {   // x,y,z < 64
-        return ((y >> 2) & 1u) | (x << 1) | ((y & 0x38u) << 4) | ((z & 0x38u) << 7);
+        // grouped for v_bfe + 3 v_lshl_or + 2 v_and (was 8 operations)
+        const uint32_t lo = (x << 1) | __builtin_amdgcn_ubfe(y, 2u, 1u);
+        const uint32_t hi = ((z & 0x38u) << 3) | (y & 0x38u);
+        return (hi << 4) | lo;
+    }
+    // Bit of an in-region voxel in its mask word, in the low 5 bits only
+    // ((y&3)<<3 | z&7 there; v_bfe and shifts read just those): one v_bfi.
+    __device__ __forceinline__ static uint32_t word_bit5(uint32_t y, uint32_t z) {
+        uint32_t r;
+        asm("v_bfi_b32 %0, 7, %1, %2" : "=v"(r) : "v"(z), "v"(y << 3));
+        return r;
     }
 
     // doesVoxelSpaceExist (StorageStructure.cuh:29-32,49-52) ->
@@ -331,6 +346,12 @@ struct Ctx {
     __device__ __forceinline__ static bool in_region_bits(f3 o) {
         const uint32_t a = __float_as_uint(o.x + 0.0f), b = __float_as_uint(o.y + 0.0f), c = __float_as_uint(o.z + 0.0f);
         return max(max(a, b), c) < 0x42800000u;
+    }
+    // For coordinates that are not -0: a walk position is canonicalised (x + 0)
+    // once, and o + p only gives a zero by exact cancellation, which rounds to
+    // +0 -- so positions stepped from it are never -0 either.
+    __device__ __forceinline__ static bool in_region_bits_nz(f3 o) {
+        return max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)) < 0x42800000u;
     }
     __device__ __forceinline__ static bool grid_in_region(int32_t a, int32_t b, int32_t c) {   // :436-439
         return (uint32_t)a < 64u && (uint32_t)b < 64u && (uint32_t)c < 64u;

@@ -134,7 +134,8 @@ struct Walker : Ctx<STORE, COUNT> {
             // single condition; the step of the hit iteration is computed and
             // discarded (the reference breaks before it).  tick() semantics are
             // kept: iteration k of the pixel runs iff k <= kIterBudget.
-            if (!this->in_region_bits(o)) return false;
+            o = add(o, f3{0.0f, 0.0f, 0.0f});      // -0 -> +0 (in_region_bits_nz below)
+            if (!this->in_region_bits_nz(o)) return false;
             if (aborted || this->iters >= kIterBudget) { aborted = true; return false; }
             bool found = false, inside = true, crawl = false;
             // crawl exits (see crawl_steps): from this iteration count on (crawl pass);
@@ -143,6 +144,8 @@ struct Walker : Ctx<STORE, COUNT> {
             bool crawl_off = false;
             uint32_t vi = 0;
             int32_t qx = 0, qy = 0, qz = 0;   // voxel of the iteration that exited to crawl
+            Blk blk{0u, kNone};
+            uint32_t bit = 0;
             for (;;) {
                 // Per-walk constants, (re)made here in the crawl pass so they are
                 // dead across the crawl code below (the barrier keeps them from
@@ -152,32 +155,36 @@ struct Walker : Ctx<STORE, COUNT> {
                 // Hoisted reciprocals (div_fast) and +-1 plane signs for the loop.
                 const Rcp rx = rcp_setup(dl.x), ry = rcp_setup(dl.y), rz = rcp_setup(dl.z);
                 const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
+                const float ex = gx * kEps, ey = gy * kEps, ez = gz * kEps;
                 const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
                 // A guarded zero direction component (shadow ray) keeps the lane on the
                 // slow branch, which applies the guard: the fast path needs no selects.
                 const bool walk_ok = rx.ok && ry.ok && rz.ok && !zx && !zy && !zz;
+                // one compare per iteration: min |n| >= lim (lim = +inf sends the lane
+                // to the slow branch every iteration; |n| < 73 inside a region)
+                const float nlim = walk_ok ? 0x1p-90f : kInf;
                 for (;;) {
                     ++this->iters;
                     const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
                     this->count(4);
                     const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
-                    Blk blk = mreg[wi];
+                    blk = mreg[wi];
                     // both candidate planes, computed while the mask word is in
                     // flight and materialised (with the whole 8-B word: one load)
-                    float vX = next_plane(o.x, gx, kEps), vY = next_plane(o.y, gy, kEps), vZ = next_plane(o.z, gz, kEps);
+                    float vX = next_plane_fma(o.x, gx, ex), vY = next_plane_fma(o.y, gy, ey), vZ = next_plane_fma(o.z, gz, ez);
                     float cX = (float)((vx & ~7) + cx8), cY = (float)((vy & ~7) + cy8), cZ = (float)((vz & ~7) + cz8);
                     asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
                     const bool skip = absent(blk);
-                    const uint32_t bit = (((uint32_t)vy & 3u) << 3) | ((uint32_t)vz & 7u);
-                    found = (!skip) & (((blk.x >> bit) & 1u) != 0u);
-                    vi = blk.y + __popc(blk.x & ((1u << bit) - 1u));
+                    bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
+                    found = (!skip) & (__builtin_amdgcn_ubfe(blk.x, bit, 1u) != 0u);
+                    vi = blk.y + __popc(blk.x & ((1u << (bit & 31u)) - 1u));
                     if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
                     nX = skip ? cX : vX;
                     nY = skip ? cY : vY;
                     nZ = skip ? cZ : vZ;
                     const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
                     float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
-                    const bool bad = !walk_ok || !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= 0x1p-90f);
+                    const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
                     crawl = false;
                     if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
                         sX = bad ? (zx ? kInf : ax / d.x) : sX;
@@ -192,13 +199,22 @@ struct Walker : Ctx<STORE, COUNT> {
                     const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
                     tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
                     const f3 on = add(o, scl(sMin + kEps, d));
-                    inside = this->in_region_bits(on);
+                    inside = this->in_region_bits_nz(on);
                     qx = vx; qy = vy; qz = vz;
                     o.x = found ? o.x : on.x;   // per component: a struct-valued ?: goes through scratch
                     o.y = found ? o.y : on.y;
                     o.z = found ? o.z : on.z;
                     if (found || !inside || this->iters >= kIterBudget || crawl) break;
                 }
+                // Why the lane left, recomputed from values the loop keeps in VGPRs
+                // anyway (a flag read after a divergent loop is carried through it as
+                // a lane mask, at three scalar ops per flag per iteration; the barrier
+                // keeps the compiler from reusing the in-loop flags): a hit leaves o
+                // unstepped (inside), and a crawl is the one remaining exit.
+                asm("" : "+v"(blk.x), "+v"(blk.y), "+v"(bit), "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(this->iters));
+                found = !absent(blk) & (__builtin_amdgcn_ubfe(blk.x, bit, 1u) != 0u);
+                inside = found || this->in_region_bits_nz(o);
+                crawl = !found && inside && this->iters < kIterBudget;
                 if (!crawl || !inside || this->iters >= kIterBudget) break;
                 if constexpr (!CRAWL) {
                     // Defer only a real crawl: an axis on its own skip plane that
@@ -240,7 +256,7 @@ struct Walker : Ctx<STORE, COUNT> {
                         o.z = o.z + fm * cw.dz;
                         this->iters += cw.m;
                         this->count(4u * cw.m);
-                        inside = this->in_region_bits(o);
+                        inside = this->in_region_bits_nz(o);
                         if (!inside || this->iters >= kIterBudget) break;
                     }
                 }
@@ -540,8 +556,11 @@ __device__ __forceinline__ void add_bytes(const KView& v, uint32_t lane, unsigne
 }
 
 // Tile pass: one lane per pixel, one wave per 8x8 tile, 2x2 tiles per workgroup.
+#ifndef VR_ORIG_WAVES
+#define VR_ORIG_WAVES 7
+#endif
 template <int STORE, int ALGO, bool COUNT>
-__global__ __launch_bounds__(256, ALGO == ALGO_ORIGINAL ? 7 : 3) void march_kernel(KScene s, KView v) {
+__global__ __launch_bounds__(256, ALGO == ALGO_ORIGINAL ? VR_ORIG_WAVES : 3) void march_kernel(KScene s, KView v) {
     __shared__ float inv255_lds[256];
     const float* inv255 = load_inv255(inv255_lds);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
