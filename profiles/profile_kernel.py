@@ -41,5 +41,8 @@ for e0, e1 in ev:
     e1.record(s)
 torch.cuda.synchronize()
 ms = [e0.elapsed_time(e1) for e0, e1 in ev]
+o64 = out.to(torch.int64)
+digest = int(((o64 & 0xFFFFFFFF) * torch.arange(1, W * H + 1, device=out.device, dtype=torch.int64)).sum()) & 0xFFFFFFFFFFFF
 print(f"{a.config} {a.kernel} {store.name} {algo.name} shadows={not a.no_shadows}: mean {np.mean(ms):.4f} ms "
-      f"min {np.min(ms):.4f} ms -> {W * H / np.mean(ms) / 1e3:.1f} Mrays/s", flush=True)
+      f"median {np.median(ms):.4f} min {np.min(ms):.4f} ms -> {W * H / np.mean(ms) / 1e3:.1f} Mrays/s "
+      f"digest {digest:012x}", flush=True)

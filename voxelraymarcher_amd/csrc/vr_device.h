@@ -100,6 +100,20 @@ __device__ __forceinline__ float next_plane_fma(float o, float s, float se) {
     return __builtin_fmaf(s, ceilf(s * o), se);
 }
 
+// (a << s) | b as one v_lshl_or_b32
+__device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t sh, uint32_t b) {
+    uint32_t r;
+    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(sh), "v"(b));
+    return r;
+}
+// m ? a : b per bit (m = 0 or ~0): one v_bfi_b32 (the compiler splits the
+// and/or form into three operations).
+__device__ __forceinline__ float bit_select(uint32_t m, float a, float b) {
+    float r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+
 // CuckooHashTable::hashFunc1 / hashFunc2 (CuckooHashTable.cuh:181-202),
 // int arithmetic with arithmetic right shifts.
 __device__ __forceinline__ uint32_t hash1(uint32_t k, uint32_t offset) {
@@ -197,10 +211,13 @@ struct Ctx {
         return s.vcs_mask + (size_t)reg * 8192u + (slot << 4);
     }
     __device__ __forceinline__ static uint32_t word_index(uint32_t x, uint32_t y, uint32_t z) {   // x,y,z < 64
-        // grouped for v_bfe + 3 v_lshl_or + 2 v_and (was 8 operations)
-        const uint32_t lo = (x << 1) | __builtin_amdgcn_ubfe(y, 2u, 1u);
-        const uint32_t hi = ((z & 0x38u) << 3) | (y & 0x38u);
-        return (hi << 4) | lo;
+        // v_bfe + 3 v_lshl_or; the two v_and (y & 0x38, z & 0x38) are shared
+        // with the cluster-skip planes of the walk
+        // (the instructions are pinned: left to itself the compiler re-associates
+        // the shifts and masks into 8 operations)
+        const uint32_t lo = lshl_or(x, 1u, __builtin_amdgcn_ubfe(y, 2u, 1u));
+        const uint32_t hi = lshl_or(z & 0x38u, 3u, y & 0x38u);
+        return lshl_or(hi, 4u, lo);
     }
     // Bit of an in-region voxel in its mask word, in the low 5 bits only
     // ((y&3)<<3 | z&7 there; v_bfe and shifts read just those): one v_bfi.

@@ -106,13 +106,20 @@ struct Walker : Ctx<STORE, COUNT> {
     // branch's are block-scoped).  One set of IEEE divisions per
     // iteration instead of two divergent ones.  Lighting is applied by the
     // caller after the walk (Hit carries colour, normal and position).
-    template <bool SHADOW>
+    // EQ (shadow walks only): the direction's components are equal (the
+    // default light, normalize(1,1,1), Main.cu:28).  Then every t_i = a_i / d
+    // shares one divisor, and correctly rounded division is monotone in the
+    // numerator, so min_i RN(a_i / d) = RN(min_i a_i / d) (max_i for d < 0):
+    // one division per iteration instead of three, and (t + EPSILON) * d_i is
+    // one product.  Bit-identical; shadow walks read no per-axis t values.
+    template <bool SHADOW, bool EQ = false>
     __device__ __forceinline__ bool grid_original(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h) {
-        return grid_original_rt(o, d, reg, cr, h, SHADOW);
+        return grid_original_rt(o, d, reg, cr, h, SHADOW, SHADOW && EQ);
     }
     // The same with the shadow flag a per-lane value (fused primary + shadow
     // walk); the template form above constant-folds it.
-    __device__ __forceinline__ bool grid_original_rt(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h, const bool SHADOW) {
+    __device__ __forceinline__ bool grid_original_rt(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h, const bool SHADOW,
+                                                     const bool EQ) {
         const bool px = d.x > 0.0f, py = d.y > 0.0f, pz = d.z > 0.0f;
         const bool zx = SHADOW && d.x == 0.0f, zy = SHADOW && d.y == 0.0f, zz = SHADOW && d.z == 0.0f;
         float nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
@@ -153,7 +160,7 @@ struct Walker : Ctx<STORE, COUNT> {
                 f3 dl = d;
                 if (CRAWL) asm("" : "+v"(dl.x), "+v"(dl.y), "+v"(dl.z));
                 // Hoisted reciprocals (div_fast) and +-1 plane signs for the loop.
-                const Rcp rx = rcp_setup(dl.x), ry = rcp_setup(dl.y), rz = rcp_setup(dl.z);
+                const Rcp rx = rcp_setup(EQ ? fabsf(dl.x) : dl.x), ry = rcp_setup(dl.y), rz = rcp_setup(dl.z);
                 const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
                 const float ex = gx * kEps, ey = gy * kEps, ez = gz * kEps;
                 const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
@@ -172,39 +179,61 @@ struct Walker : Ctx<STORE, COUNT> {
                     // both candidate planes, computed while the mask word is in
                     // flight and materialised (with the whole 8-B word: one load)
                     float vX = next_plane_fma(o.x, gx, ex), vY = next_plane_fma(o.y, gy, ey), vZ = next_plane_fma(o.z, gz, ez);
-                    float cX = (float)((vx & ~7) + cx8), cY = (float)((vy & ~7) + cy8), cZ = (float)((vz & ~7) + cz8);
+                    // (in the region v < 64, so v & ~7 == v & 0x38, the form word_index shares)
+                    float cX = (float)((vx & 0x38) + cx8), cY = (float)((vy & 0x38) + cy8), cZ = (float)((vz & 0x38) + cz8);
                     asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
                     const bool skip = absent(blk);
                     bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
-                    found = (!skip) & (__builtin_amdgcn_ubfe(blk.x, bit, 1u) != 0u);
+                    // 0 or ~0 (an absent cluster's words have no bits set)
+                    const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)blk.x, bit, 1u);
+                    found = fm != 0u;
                     vi = blk.y + __popc(blk.x & ((1u << (bit & 31u)) - 1u));
                     if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
                     nX = skip ? cX : vX;
                     nY = skip ? cY : vY;
                     nZ = skip ? cZ : vZ;
                     const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
-                    float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
-                    const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
+                    float sMin;
                     crawl = false;
-                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                        sX = bad ? (zx ? kInf : ax / d.x) : sX;
-                        sY = bad ? (zy ? kInf : ay / d.y) : sY;
-                        sZ = bad ? (zz ? kInf : az / d.z) : sZ;
-                        // a skip step with t = 0 (its plane axis has n = 0, so it is
-                        // always on this branch): the ray creeps through an empty cluster
-                        crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
-                                (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                    if (EQ) {
+                        // |a_i| / |d| = a_i / d up to the sign of a zero (t = -0 for
+                        // a = +0, d < 0), which neither the step nor the crawl test sees
+                        const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
+                        sMin = div_fast(am, rx);
+                        const bool bad = !(am >= nlim);
+                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                            sMin = bad ? am / fabsf(d.x) : sMin;
+                            crawl = bad & walk_ok & skip & (sMin == 0.0f) &
+                                    (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                        }
+                    } else {
+                        float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
+                        const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
+                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                            sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                            sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                            sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                            // a skip step with t = 0 (its plane axis has n = 0, so it is
+                            // always on this branch): the ray creeps through an empty cluster
+                            crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
+                                    (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                        }
+                        sMin = fminf(sX, fminf(sY, sZ));
+                        const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
+                        tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
                     }
-                    const float sMin = fminf(sX, fminf(sY, sZ));
-                    const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
-                    tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
-                    const f3 on = add(o, scl(sMin + kEps, d));
-                    inside = this->in_region_bits_nz(on);
+                    const f3 on = EQ ? add(o, f3{(sMin + kEps) * d.x, (sMin + kEps) * d.x, (sMin + kEps) * d.x})
+                                     : add(o, scl(sMin + kEps, d));
                     qx = vx; qy = vy; qz = vz;
-                    o.x = found ? o.x : on.x;   // per component: a struct-valued ?: goes through scratch
-                    o.y = found ? o.y : on.y;
-                    o.z = found ? o.z : on.z;
-                    if (found || !inside || this->iters >= kIterBudget || crawl) break;
+                    // a hit keeps o unstepped (bit-select on the hit mask)
+                    o.x = bit_select(fm, o.x, on.x);
+                    o.y = bit_select(fm, o.y, on.y);
+                    o.z = bit_select(fm, o.z, on.z);
+                    // One unsigned compare for hit, region exit (in_region_bits_nz of the
+                    // stepped position) and the budget (iters >= kIterBudget):
+                    const uint32_t ev = max(max(max(max(__float_as_uint(on.x), __float_as_uint(on.y)), __float_as_uint(on.z)),
+                                                this->iters + (0x42800000u - kIterBudget)), fm);
+                    if (ev >= 0x42800000u || crawl) break;
                 }
                 // Why the lane left, recomputed from values the loop keeps in VGPRs
                 // anyway (a flag read after a divergent loop is carried through it as
@@ -267,7 +296,7 @@ struct Walker : Ctx<STORE, COUNT> {
             }
             col = s.vcs_vals[vi];
         } else {
-            const Rcp rx = rcp_setup(d.x), ry = rcp_setup(d.y), rz = rcp_setup(d.z);
+            const Rcp rx = rcp_setup(EQ ? fabsf(d.x) : d.x), ry = rcp_setup(d.y), rz = rcp_setup(d.z);
             const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
             const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
             const bool walk_ok = rx.ok && ry.ok && rz.ok && !zx && !zy && !zz;
@@ -285,6 +314,15 @@ struct Walker : Ctx<STORE, COUNT> {
                 nY = skip ? (float)((vy & ~7) + cy8) : next_plane(o.y, gy, kEps);
                 nZ = skip ? (float)((vz & ~7) + cz8) : next_plane(o.z, gz, kEps);
                 const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
+                if (EQ) {                                 // see grid_original
+                    const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
+                    float sMin = div_fast(am, rx);
+                    const bool bad = !walk_ok || !(am >= 0x1p-90f);
+                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) sMin = bad ? am / fabsf(d.x) : sMin;
+                    const float st = (sMin + kEps) * d.x;
+                    o = add(o, f3{st, st, st});
+                    continue;
+                }
                 float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
                 const bool bad = !walk_ok || !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= 0x1p-90f);
                 if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
@@ -494,7 +532,7 @@ struct Walker : Ctx<STORE, COUNT> {
 
     // isInShadowOriginalRayMarch (Renderer.cuh:174-235) /
     // isInShadowRayMarchVoxelSceneLongestAxis (:633-694).
-    template <bool LONGEST>
+    template <bool LONGEST, bool EQ = false>
     __device__ __forceinline__ bool shadow(f3 o, i3 cr) {
         f3 d = ld3(v.L);
         Hit dummy;
@@ -506,7 +544,7 @@ struct Walker : Ctx<STORE, COUNT> {
                 if (!this->template skip_null<!LONGEST>(cr, o, d, reg)) return false;
             }
             bool hit = LONGEST ? grid_longest<true>(o, d, reg, cr, dummy)
-                               : grid_original<true>(o, d, reg, cr, dummy);
+                               : grid_original<true, EQ>(o, d, reg, cr, dummy);
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
@@ -541,7 +579,9 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, const
                                                       (float)(h.region.z * kBlock)));
             const uint32_t lit = w.lighting(h.col, h.n, rwp, h.so);
             if (v.use_shadows)
-                sh = h.longest ? w.template shadow<true>(h.so, h.region) : w.template shadow<false>(h.so, h.region);
+                sh = h.longest ? w.template shadow<true>(h.so, h.region)
+                     : v.L[0] == v.L[1] && v.L[1] == v.L[2] ? w.template shadow<false, true>(h.so, h.region)
+                                                            : w.template shadow<false>(h.so, h.region);
             col = lit * (uint32_t)!sh;
         }
         if (w.aborted) col = 0;
