@@ -175,7 +175,8 @@ def test_lighting_variants(c1, store, algo):
         check_frame(*c1, store, algo, 96, 96, cfg.scale, lit=lit)
 
 
-LIGHTS = [((0.0, 1.0, 0.0), (1.0, 1.0, 1.0)),        # two zero components: guarded shadow divisions
+LIGHTS = [((-1.0, -1.0, -1.0), (1.0, 1.0, 1.0)),     # equal negative components: one-division shadow walk, d < 0
+          ((0.0, 1.0, 0.0), (1.0, 1.0, 1.0)),        # two zero components: guarded shadow divisions
           ((1.0, 1.0, 0.0), (0.5, 1.0, 0.25)),       # long-axis tie x = y (strict '>' picks y)
           ((-1.0, 2.0, -0.5), (1.0, 0.75, 2.0)),     # negative steps, channel overflow clamps by truncation
           ((0.0, -1.0, 1.0), (1.0, 1.0, 1.0))]
@@ -189,7 +190,7 @@ def test_light_direction_and_color(c1, c2, store, algo):
     for i, (d, col) in enumerate(LIGHTS):
         lit = vr.setup_constant_values(light_direction=d, light_color=col)
         check_frame(*c1, store, algo, 96, 96, vr.CONFIGS["C1"].scale, lit=lit)
-        if i < 2:
+        if i < 3:
             check_frame(*c2, store, algo, 240, 136, vr.CONFIGS["C2"].scale, lit=lit, kernels=[vr.Kernel.TILE])
 
 

@@ -114,6 +114,20 @@ __device__ __forceinline__ float bit_select(uint32_t m, float a, float b) {
     return r;
 }
 
+// u32 `h % M` for a divisor fixed over a walk: minv = floor(2^32 / M) (2^32 - 1
+// for M = 1) gives q' = mulhi(h, minv) in {q - 1, q}, so r' = h - q' M is in
+// [0, 2M) and one wrap-around min finishes it.  Exact for every h and M >= 1.
+struct FastMod { uint32_t M, minv; };
+__device__ __forceinline__ FastMod fastmod_setup(uint32_t M) {
+    uint32_t q = 0xFFFFFFFFu / M;                       // floor((2^32 - 1) / M)
+    if (M != 1u && 0xFFFFFFFFu - q * M == M - 1u) ++q;  // M divides 2^32
+    return FastMod{M, q};
+}
+__device__ __forceinline__ uint32_t fastmod(uint32_t h, FastMod f) {
+    const uint32_t r = h - __umulhi(h, f.minv) * f.M;
+    return min(r, r - f.M);
+}
+
 // CuckooHashTable::hashFunc1 / hashFunc2 (CuckooHashTable.cuh:181-202),
 // int arithmetic with arithmetic right shifts.
 __device__ __forceinline__ uint32_t hash1(uint32_t k, uint32_t offset) {

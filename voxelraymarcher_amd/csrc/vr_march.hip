@@ -296,44 +296,76 @@ struct Walker : Ctx<STORE, COUNT> {
             }
             col = s.vcs_vals[vi];
         } else {
+            // Cuckoo store (doesVoxelSpaceExist is always true: no cluster skips).
+            // The region's table header is read once per walk, the two slot
+            // indices use a hoisted reciprocal for `% M`, and the step of an
+            // iteration does not depend on its lookup: both slot loads are in
+            // flight while the next position is computed, and a straight-line
+            // body ends in one exit test, as in the VCS walk above.
+            o = add(o, f3{0.0f, 0.0f, 0.0f});      // -0 -> +0 (in_region_bits_nz below)
+            if (!this->in_region_bits_nz(o)) return false;
+            if (aborted || this->iters >= kIterBudget) { aborted = true; return false; }
+            const uint4 m = s.ht_meta[reg];        // {base, M, prime, offset}
+            const FastMod fmod = fastmod_setup(m.y);
+            const uint2* t1 = s.ht_slots + m.x;
+            const uint2* t2 = t1 + m.y;
             const Rcp rx = rcp_setup(EQ ? fabsf(d.x) : d.x), ry = rcp_setup(d.y), rz = rcp_setup(d.z);
             const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
-            const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
+            const float ex = gx * kEps, ey = gy * kEps, ez = gz * kEps;
             const bool walk_ok = rx.ok && ry.ok && rz.ok && !zx && !zy && !zz;
-            while (in_region(o)) {
-                if (!tick()) return false;
-                const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-                const Blk blk = exists(reg, vx, vy, vz);
-                const bool skip = absent(blk);
-                if (!skip) {
-                    col = lookup(reg, blk, vx, vy, vz);
-                    if (col != kEmpty) break;
-                }
-                // in_region(o) => vx,vy,vz >= 0, so (v / 8) * 8 == v & ~7
-                nX = skip ? (float)((vx & ~7) + cx8) : next_plane(o.x, gx, kEps);
-                nY = skip ? (float)((vy & ~7) + cy8) : next_plane(o.y, gy, kEps);
-                nZ = skip ? (float)((vz & ~7) + cz8) : next_plane(o.z, gz, kEps);
-                const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
+            const float nlim = walk_ok ? 0x1p-90f : kInf;
+            uint32_t key = 0;
+            uint2 e1{0u, 0u}, e2{0u, 0u};
+            for (;;) {
+                ++this->iters;
+                const uint32_t vx = (uint32_t)f2i(o.x), vy = (uint32_t)f2i(o.y), vz = (uint32_t)f2i(o.z);
+                key = lshl_or(lshl_or(vx, 10u, vy), 10u, vz);              // generate3DPoint (x<<20|y<<10|z)
+                e1 = t1[fastmod(hash1(key, m.w), fmod)];
+                e2 = t2[fastmod(hash2(key, m.z), fmod)];
+                // rayMarchVoxelGrid's voxel step (Renderer.cuh:318-331), while the slots load
+                const float ax = next_plane_fma(o.x, gx, ex) - o.x, ay = next_plane_fma(o.y, gy, ey) - o.y,
+                            az = next_plane_fma(o.z, gz, ez) - o.z;
+                float sMin, sX = 0.0f, sY = 0.0f, sZ = 0.0f;
                 if (EQ) {                                 // see grid_original
                     const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
-                    float sMin = div_fast(am, rx);
-                    const bool bad = !walk_ok || !(am >= 0x1p-90f);
+                    sMin = div_fast(am, rx);
+                    const bool bad = !(am >= nlim);
                     if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) sMin = bad ? am / fabsf(d.x) : sMin;
-                    const float st = (sMin + kEps) * d.x;
-                    o = add(o, f3{st, st, st});
-                    continue;
+                } else {
+                    sX = div_fast(ax, rx); sY = div_fast(ay, ry); sZ = div_fast(az, rz);
+                    const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
+                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                        sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                        sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                        sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                    }
+                    sMin = fminf(sX, fminf(sY, sZ));
                 }
-                float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
-                const bool bad = !walk_ok || !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= 0x1p-90f);
-                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                    sX = bad ? (zx ? kInf : ax / d.x) : sX;
-                    sY = bad ? (zy ? kInf : ay / d.y) : sY;
-                    sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                const f3 on = EQ ? add(o, f3{(sMin + kEps) * d.x, (sMin + kEps) * d.x, (sMin + kEps) * d.x})
+                                 : add(o, scl(sMin + kEps, d));
+                // CuckooHashTable::lookupVoxel (CuckooHashTable.cuh:59-76): key1 (+val1 on a
+                // match), else key2 (+val2 on a match)
+                const bool m1 = e1.x == key, m2 = e2.x == key;
+                this->count(m1 ? 8u : (m2 ? 12u : 8u));
+                const uint32_t fm = (m1 | m2) ? ~0u : 0u;
+                if (!SHADOW && !EQ) {                     // a non-hit step: its t values feed the normal
+                    tX = fm ? tX : sX; tY = fm ? tY : sY; tZ = fm ? tZ : sZ; tMin = fm ? tMin : sMin;
                 }
-                const float sMin = fminf(sX, fminf(sY, sZ));
-                if (!skip) { tX = sX; tY = sY; tZ = sZ; tMin = sMin; }
-                o = add(o, scl(sMin + kEps, d));
+                o.x = bit_select(fm, o.x, on.x);
+                o.y = bit_select(fm, o.y, on.y);
+                o.z = bit_select(fm, o.z, on.z);
+                const uint32_t ev = max(max(max(max(__float_as_uint(on.x), __float_as_uint(on.y)), __float_as_uint(on.z)),
+                                            this->iters + (0x42800000u - kIterBudget)), fm);
+                if (ev >= 0x42800000u) break;
             }
+            // why the lane left (see the VCS walk): recomputed from VGPR values
+            asm("" : "+v"(e1.x), "+v"(e1.y), "+v"(e2.x), "+v"(e2.y), "+v"(key), "+v"(o.x), "+v"(o.y), "+v"(o.z));
+            const bool m1 = e1.x == key, found = m1 || e2.x == key;
+            if (!found) {
+                if (this->in_region_bits_nz(o)) aborted = true;    // budget spent inside the region
+                return false;
+            }
+            col = m1 ? e1.y : e2.y;
         }
         if (col == kEmpty) return false;
         if (!SHADOW) {
