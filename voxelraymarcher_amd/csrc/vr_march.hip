@@ -523,6 +523,184 @@ struct Walker : Ctx<STORE, COUNT> {
         return grid_original<SHADOW>(oo, od, reg, cr, h);
     }
 
+    // The VCS longest-axis walk with ONE reference loop iteration per loop
+    // iteration (rayMarchVoxelGridLongestAxis, Renderer.cuh:760-915; shadow twin
+    // :495-631; performVoxelSpaceJump :696-751 / :441-492).  A lane is either
+    //   main : one whole iteration of the reference's while loop -- its (up to
+    //          three) axis probes are known at its top (M/S in crossing order, then
+    //          L, each adding one axis of `ad` to the grid position), so their three
+    //          mask words are loaded together and evaluated in order; the first
+    //          absent cluster starts a jump, the first stored voxel is the hit, or
+    //   jump : one cluster skip of performVoxelSpaceJump and the probe of the
+    //          cell it lands in (the jump's first existence test re-reads the
+    //          probe that started it, known absent: counted, not loaded).
+    // Probes, ticks and counted bytes are the reference's, in its order; the
+    // later probes of an iteration that stops early are loaded but not counted.
+    template <bool SHADOW>
+    __device__ __forceinline__ bool grid_longest_vcs(f3& oo, f3 od, uint32_t reg, i3 cr, Hit& h) {
+        uint32_t L, M, S;
+        // Ray::convertRayToLongestAxisDirection (Ray.cuh:19-71)
+        float ax = fabsf(od.x), ay = fabsf(od.y), az = fabsf(od.z), k;
+        if (ax > ay && ax > az) {
+            L = 0; M = ay > az ? 1 : 2; S = ay > az ? 2 : 1; k = 1.0f / ax;
+        } else if (ay > az) {
+            L = 1; M = ax > az ? 0 : 2; S = ax > az ? 2 : 0; k = 1.0f / ay;
+        } else {
+            L = 2; M = ax > ay ? 0 : 1; S = ax > ay ? 1 : 0; k = 1.0f / az;
+        }
+        const f3 ds = scl(k, od);
+        f3 old_o = oo;
+        i3 g{f2i(oo.x), f2i(oo.y), f2i(oo.z)};
+        i3 ad{0, 0, 0};
+        const int32_t adL = comp(od, L) < 0.0f ? -1 : 1;
+        seti(ad, L, adL);
+        f3 ray_o;
+        {
+            // x / (float)adL with adL = +-1 is exactly x * adL
+            const float gL = (float)geti(g, L), oL = comp(oo, L);
+            const float t = adL > 0 ? (gL + kEps + 1.0f - oL) * (float)adL : (gL - kEps - oL) * (float)adL;
+            ray_o = add(old_o, scl(t, ds));
+        }
+        seti(ad, M, f2i(comp(ray_o, M)) - geti(g, M));
+        seti(ad, S, f2i(comp(ray_o, S)) - geti(g, S));
+        const bool mid_floor = comp(ds, M) < 0.0f;   // decimalToIntFunc (:784)
+        const float dsM = comp(ds, M), dsS = comp(ds, S), dsL = comp(ds, L);
+        const uint2* mreg = s.vcs_mask + (size_t)reg * 8192u;
+        float tX = 0.0f, tY = 0.0f, tZ = 0.0f, tMin = 0.0f;   // the jump's last skip (hit normal)
+        bool jumping = false;
+        for (;;) {
+            // ---- the probes of this iteration: slots 0..n-1 (slot n-1 of a main lane is g + ad)
+            i3 p0, p1, p2;
+            uint32_t n, a0 = L, a1 = L;
+            if (!jumping) {
+                p2 = i3{g.x + ad.x, g.y + ad.y, g.z + ad.z};
+                if (!grid_in_region(p2.x, p2.y, p2.z)) break;          // -> the original-DDA tail
+                if (!tick()) return false;
+                const int32_t adM = geti(ad, M), adS = geti(ad, S);
+                if (adS != 0 && adM != 0) {
+                    const float om = comp(old_o, M);
+                    const float t1 = ((mid_floor ? floorf(om) : ceilf(om)) - om) / dsM;
+                    const float sp = comp(old_o, S) + dsS * t1;
+                    const int32_t sd = f2i(floorf(sp)) - geti(g, S);
+                    a0 = sd != 0 ? S : M;
+                    a1 = sd != 0 ? M : S;
+                    n = 3;
+                } else {
+                    a0 = adM != 0 ? M : S;
+                    n = (adM | adS) != 0 ? 2u : 1u;
+                }
+                p0 = g; seti(p0, a0, geti(g, a0) + geti(ad, a0));
+                p1 = p0; seti(p1, a1, geti(p0, a1) + geti(ad, a1));
+                if (n == 2u) { p1 = p2; a1 = L; }
+                if (n == 1u) { p0 = p2; a0 = L; }
+            } else {
+                if (!tick()) return false;
+                // performVoxelSpaceJump's cluster skip (:707-725), integer planes from g
+                const int32_t nx = ds.x > 0.0f ? ((g.x / 8) + 1) * 8 : (g.x / 8) * 8;
+                const int32_t ny = ds.y > 0.0f ? ((g.y / 8) + 1) * 8 : (g.y / 8) * 8;
+                const int32_t nz = ds.z > 0.0f ? ((g.z / 8) + 1) * 8 : (g.z / 8) * 8;
+                tX = ((float)nx - old_o.x) / ds.x;
+                tY = ((float)ny - old_o.y) / ds.y;
+                tZ = ((float)nz - old_o.z) / ds.z;
+                tMin = fminf(tX, fminf(tY, tZ)) + kEps;
+                old_o = add(old_o, scl(tMin, ds));
+                g = i3{f2i(floorf(old_o.x)), f2i(floorf(old_o.y)), f2i(floorf(old_o.z))};
+                if (!grid_in_region(g.x, g.y, g.z)) {
+                    oo = old_o;
+                    return false;
+                }
+                p0 = g; p1 = g; p2 = g;
+                n = 1;
+            }
+            // ---- the mask words of all probe slots, requested together
+            const bool inr = (((uint32_t)p0.x | (uint32_t)p0.y | (uint32_t)p0.z | (uint32_t)p1.x | (uint32_t)p1.y |
+                               (uint32_t)p1.z) < 64u);   // p2 is in the region (tested above / = p0)
+            const uint32_t w0 = this->word_index((uint32_t)p0.x & 63u, (uint32_t)p0.y & 63u, (uint32_t)p0.z & 63u);
+            const uint32_t w1 = this->word_index((uint32_t)p1.x & 63u, (uint32_t)p1.y & 63u, (uint32_t)p1.z & 63u);
+            const uint32_t w2 = this->word_index((uint32_t)p2.x & 63u, (uint32_t)p2.y & 63u, (uint32_t)p2.z & 63u);
+            Blk b0 = mreg[w0], b1 = mreg[w1];
+            const Blk b2 = mreg[w2];
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(!inr) != 0, 0)) {
+                if (!inr) {       // huge grid coordinates: the general (aliasing) form
+                    b0 = this->mask_word(reg, p0.x, p0.y, p0.z);
+                    b1 = this->mask_word(reg, p1.x, p1.y, p1.z);
+                }
+            }
+            // ---- evaluate the slots in the reference's order
+            uint32_t stop = n, col = kEmpty;
+            bool hit = false;
+            auto eval = [&](uint32_t i, const i3& p, const Blk& b, uint32_t wi) {
+                if (i >= n || stop != n) return;
+                this->count(4);                       // doesVoxelSpaceExist
+                if (absent(b)) { stop = i; return; }
+                uint32_t c;
+                if (((uint32_t)p.x | (uint32_t)p.y | (uint32_t)p.z) < 64u) {
+                    const uint32_t bit = this->word_bit5((uint32_t)p.y, (uint32_t)p.z) & 31u;
+                    const bool found = (b.x >> bit) & 1u;
+                    const uint32_t vi = b.y + __popc(b.x & ((1u << bit) - 1u));
+                    if (COUNT) this->count_bsearch(mreg + (wi & ~15u), vi, found);
+                    c = found ? vi : kEmpty;          // value index (read below)
+                    if (found) { hit = true; stop = i; col = c; }
+                } else {
+                    c = this->lookup_aliased(reg, p.x, p.y, p.z);
+                    if (c != kEmpty) { hit = true; stop = i; col = c | 0x80000000u; }   // a colour, not an index
+                }
+            };
+            eval(0u, p0, b0, w0);
+            eval(1u, p1, b1, w1);
+            eval(2u, p2, b2, w2);
+            if (hit) {
+                const uint32_t v = (col & 0x80000000u) ? (col & 0x7FFFFFFFu) : s.vcs_vals[col];
+                if (!SHADOW) {
+                    h.col = v;
+                    h.region = cr;
+                    h.longest = true;
+                    if (jumping) {                   // performVoxelSpaceJump's hit
+                        h.n = normal_from_t(tX, tY, tZ, tMin, ds);
+                        h.so = old_o;
+                    } else {                         // an axis step's hit
+                        const uint32_t axis = stop == 0u ? a0 : (stop == 1u ? a1 : L);
+                        f3 nn = mk(0.0f, 0.0f, 0.0f);
+                        setf(nn, axis, copysignf(1.0f, -comp(ds, axis)));
+                        h.n = nn;
+                        if (axis == L) {
+                            h.so = ray_o;
+                        } else {                     // getLocalHitLocation (Renderer.cuh:753-758)
+                            const float o = comp(old_o, axis), dd = comp(ds, axis);
+                            const float t = dd > 0.0f ? (ceilf(o) - o) / dd : (floorf(o) - o) / dd;
+                            h.so = add(old_o, scl(t, ds));
+                        }
+                    }
+                }
+                return true;
+            }
+            if (jumping) {
+                if (stop == 0u) continue;            // still no cluster: skip again
+                // landed in an existing cluster without a hit: CONTINUE_VAL (:740-750)
+                const float oL = comp(old_o, L);
+                const float tNext = dsL > 0.0f ? (ceilf(oL) - oL) / dsL : (floorf(oL) - oL) / dsL;
+                ray_o = add(old_o, scl(tNext + kEps, ds));
+                seti(ad, M, f2i(comp(ray_o, M)) - geti(g, M));
+                seti(ad, S, f2i(comp(ray_o, S)) - geti(g, S));
+                jumping = false;
+                continue;
+            }
+            if (stop != n) {                         // an absent cluster: performVoxelSpaceJump
+                g = stop == 0u ? p0 : (stop == 1u ? p1 : p2);
+                this->count(4);                      // its first existence test (this same cell)
+                jumping = true;
+                continue;
+            }
+            g = p2;                                  // end of the iteration (:903-906)
+            old_o = ray_o;
+            ray_o = add(ray_o, ds);
+            seti(ad, M, f2i(comp(ray_o, M)) - geti(g, M));
+            seti(ad, S, f2i(comp(ray_o, S)) - geti(g, S));
+        }
+        oo = old_o;     // Renderer.cuh:912 (direction of originalRay kept)
+        return grid_original<SHADOW>(oo, od, reg, cr, h);
+    }
+
     // rayMarchVoxelScene (Renderer.cuh:338-434) / rayMarchVoxelSceneLongestAxis (:917-1010).
     template <int ALGO>
     __device__ __forceinline__ bool primary(f3 wo, f3 wd, Hit& h) {
@@ -554,7 +732,8 @@ struct Walker : Ctx<STORE, COUNT> {
                 if (!this->template skip_null<false>(cr, o, d, reg)) return false;
             }
             bool hit = ALGO == ALGO_ORIGINAL ? grid_original<false>(o, d, reg, cr, h)
-                                             : grid_longest<false>(o, d, reg, cr, h);
+                                             : (STORE == STORE_VCS ? grid_longest_vcs<false>(o, d, reg, cr, h)
+                                                                   : grid_longest<false>(o, d, reg, cr, h));
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
@@ -575,7 +754,8 @@ struct Walker : Ctx<STORE, COUNT> {
                 if (!tick()) return false;
                 if (!this->template skip_null<!LONGEST>(cr, o, d, reg)) return false;
             }
-            bool hit = LONGEST ? grid_longest<true>(o, d, reg, cr, dummy)
+            bool hit = LONGEST ? (STORE == STORE_VCS ? grid_longest_vcs<true>(o, d, reg, cr, dummy)
+                                                     : grid_longest<true>(o, d, reg, cr, dummy))
                                : grid_original<true, EQ>(o, d, reg, cr, dummy);
             if (aborted) return false;
             if (hit) return true;
