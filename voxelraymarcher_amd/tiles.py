@@ -69,6 +69,12 @@ class BandGather:
         self.frame = (torch.empty((self.per * nranks * band_rows, width), dtype=torch.int32, device=device)
                       if rank == 0 else None)
         self.work = [None] * depth
+        # rank 0 on GPUs: the un-interleaving copy runs on a side stream, beside the
+        # next frame's render (the render is latency-bound, the copy HBM-bound); a
+        # receive buffer is gathered into again only after its copy has finished.
+        dev = torch.device(device)
+        self.side = torch.cuda.Stream(dev) if (rank == 0 and nranks > 1 and dev.type == "cuda") else None
+        self.copied = [None] * depth
         self.pending = []            # slots in submission order
         self.on_frame = on_frame     # rank 0: callback(frame[:H]) after each assembled frame
         self.k = 0
@@ -78,13 +84,23 @@ class BandGather:
             if self.on_frame is not None:
                 self.on_frame(self.bufs[slot].view(-1, self.W)[:self.H])
         else:
-            self.work[slot].wait()
+            self.work[slot].wait()          # the current stream: bufs[slot] may be rendered into again
             self.work[slot] = None
             if self.rank == 0:
                 src = self.recv[slot].view(self.R, self.per, self.B, self.W).permute(1, 0, 2, 3)
-                self.frame.view(self.per, self.R, self.B, self.W).copy_(src)
-                if self.on_frame is not None:
-                    self.on_frame(self.frame[:self.H])
+                if self.side is not None:
+                    self.side.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(self.side):
+                        self.frame.view(self.per, self.R, self.B, self.W).copy_(src)
+                        if self.on_frame is not None:
+                            self.on_frame(self.frame[:self.H])
+                        ev = torch.cuda.Event()
+                        ev.record(self.side)
+                    self.copied[slot] = ev
+                else:
+                    self.frame.view(self.per, self.R, self.B, self.W).copy_(src)
+                    if self.on_frame is not None:
+                        self.on_frame(self.frame[:self.H])
         self.pending.remove(slot)
 
     def step(self, render) -> None:
@@ -95,6 +111,9 @@ class BandGather:
         if self.R > 1:
             import torch.distributed as dist
             dst = list(self.recv[slot].unbind(0)) if self.rank == 0 else None
+            if self.copied[slot] is not None:       # its previous frame has left recv[slot]
+                torch.cuda.current_stream().wait_event(self.copied[slot])
+                self.copied[slot] = None
             self.work[slot] = dist.gather(self.bufs[slot], dst, dst=0, async_op=True)
         self.pending.append(slot)
         self.k += 1
@@ -102,3 +121,5 @@ class BandGather:
     def drain(self) -> None:
         while self.pending:
             self._finish(self.pending[0])
+        if self.side is not None:                    # the last copies complete before the frame is read
+            torch.cuda.current_stream().wait_stream(self.side)
