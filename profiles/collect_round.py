@@ -36,9 +36,34 @@ def main():
                 f"rocprofv3 --pmc passes (rocprof avg duration {tj['rocprof_avg_ns'] / 1e3:.1f} us)\n")
         for k in sorted(agg):
             f.write(f"{k:32s} {sum(agg[k]) / len(agg[k]):.6g}\n")
+    bench = None
     if len(sys.argv) > 3:
         line = [l for l in open(sys.argv[3]) if l.startswith("{")][-1]
-        json.dump(json.loads(line), open(os.path.join(dst, "bench.json"), "w"), indent=1)
+        bench = json.loads(line)
+        json.dump(bench, open(os.path.join(dst, "bench.json"), "w"), indent=1)
+    # bench.py's phases in the kernel trace: warmup (pipelined), the isolated
+    # event loop, the timed loop (frames in flight).  Per-dispatch durations of
+    # the isolated phase vs the timed phase's dispatch throughput (span / count).
+    trace = os.path.join(run, "bench_trace", "bench_kernel_trace.csv")
+    rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(trace))
+                  if r["Kernel_Name"] == tj["kernel"])
+    steps = int(bench["steps"]) if bench else 20
+    if len(rows) >= 2 * steps:
+        iso = rows[-2 * steps:-steps]
+        timed = rows[-steps:]
+        iso_us = sum(e - b for b, e in iso) / len(iso) / 1e3
+        span_us = (max(e for _, e in timed) - timed[0][0]) / len(timed) / 1e3
+        dur_us = sum(e - b for b, e in timed) / len(timed) / 1e3
+        overlap = sum(1 for (b1, e1), (b2, e2) in zip(timed, timed[1:]) if b2 < e1)
+        with open(os.path.join(dst, "dispatch_throughput.txt"), "w") as f:
+            f.write(f"rocprofv3 kernel trace of bench.py, kernel {tj['kernel']}\n"
+                    f"isolated phase ({len(iso)} dispatches, one at a time): mean duration {iso_us:.1f} us\n"
+                    f"timed phase ({len(timed)} dispatches, frames in flight): span / dispatches {span_us:.1f} us, "
+                    f"mean duration {dur_us:.1f} us, {overlap} of {len(timed) - 1} consecutive pairs overlap\n")
+            if bench:
+                f.write(f"bench.py: kernel_ms {bench['kernel_ms'] * 1e3:.1f} us (isolated), "
+                        f"ms_per_step {bench['ms_per_step'] * 1e3:.1f} us (timed loop, wall clock)\n")
+        print(open(os.path.join(dst, "dispatch_throughput.txt")).read())
     print(open(os.path.join(dst, f"pmc_bench_{tj['config']}.txt")).read())
 
 

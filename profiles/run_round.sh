@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 BENCH="python3 bench.py --config $CFG --no-cpu-baseline"
 run() { timeout -k 10 400 "$@" >> "$OUT/log.txt" 2>&1; local rc=$?; if [ $rc -ne 0 ]; then echo "step failed rc=$rc: $*"; exit $rc; fi; }
-run rocprofv3 --kernel-trace --stats -f csv -d "$OUT/bench_trace" -o bench -- $BENCH --steps 20 --warmup 3
+run rocprofv3 --kernel-trace --stats -f csv -d "$OUT/bench_trace" -o bench -- $BENCH
 run rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d "$OUT/pmc_fetch" -o bench -- $BENCH --steps 3 --warmup 1
 run rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d "$OUT/pmc_write" -o bench -- $BENCH --steps 3 --warmup 1
 run rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -f csv -d "$OUT/pmc_sq" -o bench -- $BENCH --steps 3 --warmup 1

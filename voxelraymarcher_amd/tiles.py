@@ -5,6 +5,7 @@ gather of the framebuffer to rank 0.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -46,15 +47,19 @@ def weak_scaled_resolution(width: int, height: int, nranks: int) -> tuple[int, i
 
 
 class BandGather:
-    """Row-band image tiling across ranks with the gather to rank 0 overlapped.
+    """Row-band image tiling across ranks, with frames in flight.
 
     step(render) renders this rank's bands of the next frame into one of `depth`
     band buffers and starts an asynchronous gather of it to rank 0 (RCCL on
-    GPUs, gloo on CPU); the buffer is reused `depth` frames later, after that
-    gather has completed, and rank 0 then assembles the frame into `frame`
-    (one permuting copy).  So frame k's gather runs beside frame k+1's render.
-    drain() completes every outstanding frame.  With one rank the band buffer
-    already is the frame (bands in row order) and nothing is exchanged.
+    GPUs, gloo on CPU); rank 0 then assembles the frame into `frame` (one
+    permuting copy).  On GPUs every buffer slot has its own stream: the render of
+    frame k+1 does not wait for frame k (the few long waves that end a frame
+    overlap the start of the next one), frame k's gather runs beside frame k+1's
+    render, and rank 0's assembly copies run on a side stream beside both.  A
+    slot is reused `depth` frames later, after its gather (and, on rank 0, its
+    copy) has completed.  drain() completes every outstanding frame and joins
+    all streams into the caller's.  With one rank the band buffer already is
+    the frame (bands in row order) and nothing is exchanged.
     """
 
     def __init__(self, width: int, height: int, band_rows: int, rank: int, nranks: int,
@@ -69,57 +74,74 @@ class BandGather:
         self.frame = (torch.empty((self.per * nranks * band_rows, width), dtype=torch.int32, device=device)
                       if rank == 0 else None)
         self.work = [None] * depth
-        # rank 0 on GPUs: the un-interleaving copy runs on a side stream, beside the
-        # next frame's render (the render is latency-bound, the copy HBM-bound); a
-        # receive buffer is gathered into again only after its copy has finished.
         dev = torch.device(device)
-        self.side = torch.cuda.Stream(dev) if (rank == 0 and nranks > 1 and dev.type == "cuda") else None
+        cuda = dev.type == "cuda"
+        self.streams = [torch.cuda.Stream(dev) for _ in range(depth)] if cuda else None
+        # rank 0: the un-interleaving copy on a side stream (the render is latency-bound,
+        # the copy HBM-bound); a receive buffer is gathered into again only after its
+        # copy has finished.
+        self.side = torch.cuda.Stream(dev) if (cuda and rank == 0 and nranks > 1) else None
         self.copied = [None] * depth
         self.pending = []            # slots in submission order
         self.on_frame = on_frame     # rank 0: callback(frame[:H]) after each assembled frame
         self.k = 0
 
+    def _slot_stream(self, slot: int):
+        return torch.cuda.stream(self.streams[slot]) if self.streams is not None else contextlib.nullcontext()
+
+    def _assemble(self, slot: int) -> None:
+        src = self.recv[slot].view(self.R, self.per, self.B, self.W).permute(1, 0, 2, 3)
+        self.frame.view(self.per, self.R, self.B, self.W).copy_(src)
+        if self.on_frame is not None:
+            self.on_frame(self.frame[:self.H])
+
     def _finish(self, slot: int) -> None:
-        if self.R == 1:
-            if self.on_frame is not None:
-                self.on_frame(self.bufs[slot].view(-1, self.W)[:self.H])
-        else:
-            self.work[slot].wait()          # the current stream: bufs[slot] may be rendered into again
-            self.work[slot] = None
-            if self.rank == 0:
-                src = self.recv[slot].view(self.R, self.per, self.B, self.W).permute(1, 0, 2, 3)
-                if self.side is not None:
-                    self.side.wait_stream(torch.cuda.current_stream())
-                    with torch.cuda.stream(self.side):
-                        self.frame.view(self.per, self.R, self.B, self.W).copy_(src)
-                        if self.on_frame is not None:
-                            self.on_frame(self.frame[:self.H])
-                        ev = torch.cuda.Event()
-                        ev.record(self.side)
-                    self.copied[slot] = ev
-                else:
-                    self.frame.view(self.per, self.R, self.B, self.W).copy_(src)
-                    if self.on_frame is not None:
-                        self.on_frame(self.frame[:self.H])
+        with self._slot_stream(slot):
+            if self.R == 1:
+                if self.on_frame is not None:
+                    self.on_frame(self.bufs[slot].view(-1, self.W)[:self.H])
+            else:
+                self.work[slot].wait()      # the slot's stream: bufs[slot] may be rendered into again
+                self.work[slot] = None
+                if self.rank == 0:
+                    if self.side is not None:
+                        self.side.wait_stream(self.streams[slot])
+                        with torch.cuda.stream(self.side):
+                            self._assemble(slot)
+                            ev = torch.cuda.Event()
+                            ev.record(self.side)
+                        self.copied[slot] = ev
+                    else:
+                        self._assemble(slot)
         self.pending.remove(slot)
 
     def step(self, render) -> None:
+        """render(buf) enqueues this rank's bands on the current stream."""
         slot = self.k % self.depth
         if slot in self.pending:
             self._finish(slot)
-        render(self.bufs[slot])
-        if self.R > 1:
-            import torch.distributed as dist
-            dst = list(self.recv[slot].unbind(0)) if self.rank == 0 else None
-            if self.copied[slot] is not None:       # its previous frame has left recv[slot]
-                torch.cuda.current_stream().wait_event(self.copied[slot])
-                self.copied[slot] = None
-            self.work[slot] = dist.gather(self.bufs[slot], dst, dst=0, async_op=True)
+        if self.streams is not None:
+            # the slot's stream picks up after the caller's work (inputs, earlier frames' users)
+            self.streams[slot].wait_stream(torch.cuda.current_stream()) if self.k < self.depth else None
+        with self._slot_stream(slot):
+            render(self.bufs[slot])
+            if self.R > 1:
+                import torch.distributed as dist
+                dst = list(self.recv[slot].unbind(0)) if self.rank == 0 else None
+                if self.copied[slot] is not None:       # its previous frame has left recv[slot]
+                    torch.cuda.current_stream().wait_event(self.copied[slot])
+                    self.copied[slot] = None
+                self.work[slot] = dist.gather(self.bufs[slot], dst, dst=0, async_op=True)
         self.pending.append(slot)
         self.k += 1
 
     def drain(self) -> None:
         while self.pending:
             self._finish(self.pending[0])
-        if self.side is not None:                    # the last copies complete before the frame is read
-            torch.cuda.current_stream().wait_stream(self.side)
+        if self.streams is not None:                 # the caller's stream sees every frame complete
+            cur = torch.cuda.current_stream()
+            for st in self.streams:
+                cur.wait_stream(st)
+            if self.side is not None:
+                cur.wait_stream(self.side)
+        self.k = 0
