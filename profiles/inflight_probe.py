@@ -4,7 +4,7 @@
 device synchronisation.  S = 1 is the serial frame loop; S > 1 lets the tail of
 frame i (a few long waves) overlap the start of frame i+1.  Prints frames/s,
 Mrays/s and whether every frame equals the serial frame.
-  python profiles/inflight_probe.py [C2] [K]"""
+  python profiles/inflight_probe.py [C2] [K] [tile|persistent]"""
 import os
 import sys
 import time
@@ -16,6 +16,7 @@ import voxelraymarcher_amd as vr  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "C2"
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 60
+kern = {"tile": vr.Kernel.TILE, "persistent": vr.Kernel.PERSISTENT}[sys.argv[3] if len(sys.argv) > 3 else "tile"]
 cfg = vr.CONFIGS[name]
 xyz, rgb = cfg.voxels()
 scene = vr.create_scene(xyz, rgb, cfg.store)
@@ -33,9 +34,10 @@ for S in (1, 2, 3, 4):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(K):
-            vr.run_raymarching_kernel(scene, cfg.algorithm, cam, lit, info, W, H, outs[i % S], stream=streams[i % S])
+            vr.run_raymarching_kernel(scene, cfg.algorithm, cam, lit, info, W, H, outs[i % S], stream=streams[i % S],
+                                      kernel=kern)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
     ok = all(torch.equal(o, ref) for o in outs)
-    print(f"{name} streams={S}: {dt / K * 1e3:.4f} ms/frame, {K / dt:.0f} frames/s, "
+    print(f"{name} {kern.name} streams={S}: {dt / K * 1e3:.4f} ms/frame, {K / dt:.0f} frames/s, "
           f"{W * H * K / dt / 1e6:.0f} Mrays/s, frames equal: {ok}", flush=True)
