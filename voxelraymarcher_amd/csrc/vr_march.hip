@@ -811,8 +811,11 @@ __device__ __forceinline__ void add_bytes(const KView& v, uint32_t lane, unsigne
 #ifndef VR_ORIG_WAVES
 #define VR_ORIG_WAVES 7
 #endif
+#ifndef VR_LONG_WAVES
+#define VR_LONG_WAVES 3
+#endif
 template <int STORE, int ALGO, bool COUNT>
-__global__ __launch_bounds__(256, ALGO == ALGO_ORIGINAL ? VR_ORIG_WAVES : 3) void march_kernel(KScene s, KView v) {
+__global__ __launch_bounds__(256, ALGO == ALGO_ORIGINAL ? VR_ORIG_WAVES : VR_LONG_WAVES) void march_kernel(KScene s, KView v) {
     __shared__ float inv255_lds[256];
     const float* inv255 = load_inv255(inv255_lds);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
