@@ -88,6 +88,23 @@ __device__ __forceinline__ Crawl crawl_steps(f3 on, f3 d, int32_t vx, int32_t vy
     return r;
 }
 
+// Direction-sign specialisation of the VCS loop: S = +1 / -1 a sign every lane
+// of the wave shares, 0 = per lane.  plane_v is px ? ceilf(o) + EPSILON :
+// floorf(o) - EPSILON (next_plane_fma's value); plane_c8 the cluster-skip offset.
+template <int S> struct Sgn { static constexpr int value = S; };
+template <int S>
+__device__ __forceinline__ float plane_v(float o, float g, float ge) {
+    if constexpr (S > 0) return ceilf(o) + kEps;
+    else if constexpr (S < 0) return floorf(o) - kEps;
+    else return next_plane_fma(o, g, ge);
+}
+template <int S>
+__device__ __forceinline__ int32_t plane_c8(int32_t c8) {
+    if constexpr (S > 0) return 8;
+    else if constexpr (S < 0) return 0;
+    else return c8;
+}
+
 // CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
 // crawling ray reserves an entry in the launch's deferral list and unwinds.
 template <int STORE, bool COUNT, bool CRAWL>
@@ -170,70 +187,95 @@ struct Walker : Ctx<STORE, COUNT> {
                 // one compare per iteration: min |n| >= lim (lim = +inf sends the lane
                 // to the slow branch every iteration; |n| < 73 inside a region)
                 const float nlim = walk_ok ? 0x1p-90f : kInf;
-                for (;;) {
-                    ++this->iters;
-                    const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-                    this->count(4);
-                    const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
-                    blk = mreg[wi];
-                    // both candidate planes, computed while the mask word is in
-                    // flight and materialised (with the whole 8-B word: one load)
-                    float vX = next_plane_fma(o.x, gx, ex), vY = next_plane_fma(o.y, gy, ey), vZ = next_plane_fma(o.z, gz, ez);
-                    // (in the region v < 64, so v & ~7 == v & 0x38, the form word_index shares)
-                    float cX = (float)((vx & 0x38) + cx8), cY = (float)((vy & 0x38) + cy8), cZ = (float)((vz & 0x38) + cz8);
-                    asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
-                    const bool skip = absent(blk);
-                    bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
-                    // 0 or ~0 (an absent cluster's words have no bits set)
-                    const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)blk.x, bit, 1u);
-                    found = fm != 0u;
-                    vi = blk.y + __popc(blk.x & ((1u << (bit & 31u)) - 1u));
-                    if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
-                    nX = skip ? cX : vX;
-                    nY = skip ? cY : vY;
-                    nZ = skip ? cZ : vZ;
-                    const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
-                    float sMin;
-                    crawl = false;
-                    if (EQ) {
-                        // |a_i| / |d| = a_i / d up to the sign of a zero (t = -0 for
-                        // a = +0, d < 0), which neither the step nor the crawl test sees
-                        const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
-                        sMin = div_fast(am, rx);
-                        const bool bad = !(am >= nlim);
-                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                            sMin = bad ? am / fabsf(d.x) : sMin;
-                            crawl = bad & walk_ok & skip & (sMin == 0.0f) &
-                                    (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                // The loop, specialised for a wave whose lanes share the signs of the
+                // direction (nearly every primary tile; every shadow walk): the planes
+                // then need no sign multiplications (see plane_v / plane_c8).
+                auto walk = [&](auto SXc, auto SYc, auto SZc) {
+                    constexpr int SX = decltype(SXc)::value, SY = decltype(SYc)::value, SZ = decltype(SZc)::value;
+                    for (;;) {
+                        ++this->iters;
+                        const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
+                        this->count(4);
+                        const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
+                        blk = mreg[wi];
+                        // both candidate planes, computed while the mask word is in
+                        // flight and materialised (with the whole 8-B word: one load)
+                        float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey), vZ = plane_v<SZ>(o.z, gz, ez);
+                        // (in the region v < 64, so v & ~7 == v & 0x38, the form word_index shares)
+                        float cX = (float)((vx & 0x38) + plane_c8<SX>(cx8)), cY = (float)((vy & 0x38) + plane_c8<SY>(cy8)),
+                              cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
+                        asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
+                        const bool skip = absent(blk);
+                        bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
+                        // 0 or ~0 (an absent cluster's words have no bits set)
+                        const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)blk.x, bit, 1u);
+                        found = fm != 0u;
+                        vi = blk.y + __popc(blk.x & ((1u << (bit & 31u)) - 1u));
+                        if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
+                        nX = skip ? cX : vX;
+                        nY = skip ? cY : vY;
+                        nZ = skip ? cZ : vZ;
+                        const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
+                        float sMin;
+                        crawl = false;
+                        if (EQ) {
+                            // |a_i| / |d| = a_i / d up to the sign of a zero (t = -0 for
+                            // a = +0, d < 0), which neither the step nor the crawl test sees
+                            const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
+                            sMin = div_fast(am, rx);
+                            const bool bad = !(am >= nlim);
+                            if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                                sMin = bad ? am / fabsf(d.x) : sMin;
+                                crawl = bad & walk_ok & skip & (sMin == 0.0f) &
+                                        (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                            }
+                        } else {
+                            float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
+                            const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
+                            if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                                sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                                sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                                sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                                // a skip step with t = 0 (its plane axis has n = 0, so it is
+                                // always on this branch): the ray creeps through an empty cluster
+                                crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
+                                        (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                            }
+                            sMin = fminf(sX, fminf(sY, sZ));
+                            const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
+                            tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
                         }
-                    } else {
-                        float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
-                        const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
-                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                            sX = bad ? (zx ? kInf : ax / d.x) : sX;
-                            sY = bad ? (zy ? kInf : ay / d.y) : sY;
-                            sZ = bad ? (zz ? kInf : az / d.z) : sZ;
-                            // a skip step with t = 0 (its plane axis has n = 0, so it is
-                            // always on this branch): the ray creeps through an empty cluster
-                            crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
-                                    (CRAWL ? this->iters >= crawl_after : !crawl_off);
-                        }
-                        sMin = fminf(sX, fminf(sY, sZ));
-                        const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
-                        tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
+                        const f3 on = EQ ? add(o, f3{(sMin + kEps) * d.x, (sMin + kEps) * d.x, (sMin + kEps) * d.x})
+                                         : add(o, scl(sMin + kEps, d));
+                        qx = vx; qy = vy; qz = vz;
+                        // a hit keeps o unstepped (bit-select on the hit mask)
+                        o.x = bit_select(fm, o.x, on.x);
+                        o.y = bit_select(fm, o.y, on.y);
+                        o.z = bit_select(fm, o.z, on.z);
+                        // One unsigned compare for hit, region exit (in_region_bits_nz of the
+                        // stepped position) and the budget (iters >= kIterBudget):
+                        const uint32_t ev = max(max(max(max(__float_as_uint(on.x), __float_as_uint(on.y)), __float_as_uint(on.z)),
+                                                    this->iters + (0x42800000u - kIterBudget)), fm);
+                        if (ev >= 0x42800000u || crawl) break;
                     }
-                    const f3 on = EQ ? add(o, f3{(sMin + kEps) * d.x, (sMin + kEps) * d.x, (sMin + kEps) * d.x})
-                                     : add(o, scl(sMin + kEps, d));
-                    qx = vx; qy = vy; qz = vz;
-                    // a hit keeps o unstepped (bit-select on the hit mask)
-                    o.x = bit_select(fm, o.x, on.x);
-                    o.y = bit_select(fm, o.y, on.y);
-                    o.z = bit_select(fm, o.z, on.z);
-                    // One unsigned compare for hit, region exit (in_region_bits_nz of the
-                    // stepped position) and the budget (iters >= kIterBudget):
-                    const uint32_t ev = max(max(max(max(__float_as_uint(on.x), __float_as_uint(on.y)), __float_as_uint(on.z)),
-                                                this->iters + (0x42800000u - kIterBudget)), fm);
-                    if (ev >= 0x42800000u || crawl) break;
+                };
+                const uint32_t sg = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
+                const uint32_t sg0 = __builtin_amdgcn_readfirstlane(sg);
+                using N = Sgn<-1>;
+                using P = Sgn<1>;
+                if (!CRAWL && __builtin_amdgcn_ballot_w64(sg != sg0) == 0 && (!EQ || sg0 == 0u || sg0 == 7u)) {
+                    switch (sg0) {
+                    case 0: walk(N{}, N{}, N{}); break;
+                    case 7: walk(P{}, P{}, P{}); break;
+                    case 1: if (!EQ) walk(P{}, N{}, N{}); break;
+                    case 2: if (!EQ) walk(N{}, P{}, N{}); break;
+                    case 3: if (!EQ) walk(P{}, P{}, N{}); break;
+                    case 4: if (!EQ) walk(N{}, N{}, P{}); break;
+                    case 5: if (!EQ) walk(P{}, N{}, P{}); break;
+                    default: if (!EQ) walk(N{}, P{}, P{}); break;
+                    }
+                } else {
+                    walk(Sgn<0>{}, Sgn<0>{}, Sgn<0>{});
                 }
                 // Why the lane left, recomputed from values the loop keeps in VGPRs
                 // anyway (a flag read after a divergent loop is carried through it as
