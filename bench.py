@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="C2", choices=sorted(vr.CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--frames-in-flight", type=int, default=2,
+                   help="band buffers/streams of the frame pipeline (1 = one frame at a time, for PMC passes)")
     p.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (default min(16, cpus))")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (written by profiles/collect_traffic.py)")
@@ -109,7 +111,7 @@ def main():
     lit = vr.setup_constant_values()
     info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
     stream = torch.cuda.current_stream()
-    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=2)
+    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=args.frames_in_flight)
 
     def render(buf):   # on the current stream (BandGather's slot stream in the loops)
         vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, rank, world, buf)
