@@ -155,8 +155,10 @@ uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_row
 typedef enum {
     VR_KERNEL_AUTO = 0,         /* the fastest measured for the (store, algorithm) pair */
     VR_KERNEL_TILE = 1,         /* one lane per pixel, one wave per 8x8 tile (vr_march.hip) */
-    VR_KERNEL_PERSISTENT = 2    /* persistent state machine: one voxel probe per lane-iteration,
+    VR_KERNEL_PERSISTENT = 2,   /* persistent state machine: one voxel probe per lane-iteration,
                                    primary + shadow rays fused, tile queue (vr_persist.hip) */
+    VR_KERNEL_TILE_REWALK = 3   /* the tile kernel whose crawl pass walks every deferred pixel
+                                   from its start instead of resuming it (cross-check) */
 } vr_kernel;
 
 /* Full-control render (the other vr_render* calls are wrappers of this):

@@ -95,15 +95,19 @@ def test_c5_crawl_rows():
     """C5 rows 696-712: thousands of rays that creep through empty clusters by
     RN(EPSILON * d) per iteration (o pinned on a cluster plane), most of
     them until the 65 536-iteration budget -- including a ties-to-even crawl at
-    (792, 709).  The tile pass defers them and the crawl pass fast-forwards them;
+    (792, 709).  The tile pass defers them (with the walk's state at the crawl) and
+    the crawl pass resumes and fast-forwards them;
     pixels and algorithmic bytes must still equal the oracle's plain walk."""
     cfg = vr.CONFIGS["C5"]
     xyz, rgb = cfg.voxels()
     g = vr.create_scene(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE)
     o = oracle.Scene(xyz, rgb, 0)
     for algo in ALGOS:
+        # TILE resumes each deferred crawl from its record; TILE_REWALK walks the pixel
+        # from its start (the fallback for crawls whose voxel the record cannot pin)
         check_frame(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE, algo, cfg.width, cfg.height, cfg.scale,
-                    row_begin=696, row_end=712, oracle_scene=o, gpu_scene=g)
+                    row_begin=696, row_end=712, oracle_scene=o, gpu_scene=g,
+                    kernels=KERNELS + [vr.Kernel.TILE_REWALK])
 
 
 def test_count_variant_pixels_identical(c2):

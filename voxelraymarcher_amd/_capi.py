@@ -48,7 +48,7 @@ class VrSynthParams(ctypes.Structure):
                 ("seed", c_uint64)]
 
 
-VR_KERNEL_AUTO, VR_KERNEL_TILE, VR_KERNEL_PERSISTENT = 0, 1, 2
+VR_KERNEL_AUTO, VR_KERNEL_TILE, VR_KERNEL_PERSISTENT, VR_KERNEL_TILE_REWALK = 0, 1, 2, 3
 
 
 class VrRenderOpts(ctypes.Structure):
@@ -125,6 +125,6 @@ def f3(v) -> ctypes.Array:
     return (c_float * 3)(*[float(x) for x in v])
 
 
-__all__ = ["lib", "check", "VrCamera", "VrLighting", "VrRenderOpts", "VR_KERNEL_AUTO", "VR_KERNEL_PERSISTENT", "VR_KERNEL_TILE", "VrSceneInfo", "VrSynthParams", "VrError", "SIGNATURES",
+__all__ = ["lib", "check", "VrCamera", "VrLighting", "VrRenderOpts", "VR_KERNEL_AUTO", "VR_KERNEL_PERSISTENT", "VR_KERNEL_TILE", "VR_KERNEL_TILE_REWALK", "VrSceneInfo", "VrSynthParams", "VrError", "SIGNATURES",
            "VR_STORE_VCS", "VR_STORE_HASHTABLE", "VR_ALGO_LONGESTAXIS", "VR_ALGO_ORIGINAL", "f3", "LIB_PATH",
            "c_uint8"]

@@ -202,6 +202,14 @@ struct Ctx {
         return s.region_slot[ux + uy * s.D + uz * s.D * s.D];
     }
 
+    // the same slot read again, not counted (the walk that resumes a deferred
+    // crawl already paid for it)
+    __device__ __forceinline__ uint32_t region_at_nocount(i3 r) const {
+        uint32_t mc = (uint32_t)s.min_coord;
+        uint32_t ux = (uint32_t)r.x - mc, uy = (uint32_t)r.y - mc, uz = (uint32_t)r.z - mc;
+        return s.region_slot[ux + uy * s.D + uz * s.D * s.D];
+    }
+
     // `short` getVoxelClusterID (VoxelClusterStore.cuh:21-24); -1 = past the
     // reference's 512-entry directory (no cluster).
     __device__ __forceinline__ static int32_t cluster_id(int32_t x, int32_t y, int32_t z) {

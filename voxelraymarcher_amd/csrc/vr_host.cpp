@@ -502,6 +502,8 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void*
     const bool count = v.bytes != nullptr;
     hipError_t e;
     if (kernel == VR_KERNEL_AUTO) kernel = VR_KERNEL_TILE;   // measured fastest for every pair
+    v.crawl_rewalk = kernel == VR_KERNEL_TILE_REWALK ? 1u : 0u;
+    if (kernel == VR_KERNEL_TILE_REWALK) kernel = VR_KERNEL_TILE;
     if (kernel == VR_KERNEL_TILE) {
         if (s->store == VR_STORE_VCS) {           // cluster-skip crawls: deferred to a second pass
             int rc = defer_slot(s->device, &v.defer);
@@ -811,7 +813,7 @@ int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr
     if (!out_dev) return fail(VR_E_INVALID, "out_dev is NULL");
     if (opts->row_begin > opts->row_end || opts->row_end > height) return fail(VR_E_INVALID, "bad row range");
     if (!opts->nranks || opts->rank >= opts->nranks) return fail(VR_E_INVALID, "bad band partition");
-    if (opts->kernel > VR_KERNEL_PERSISTENT) return fail(VR_E_INVALID, "unknown kernel");
+    if (opts->kernel > VR_KERNEL_TILE_REWALK) return fail(VR_E_INVALID, "unknown kernel");
     const uint32_t rows = opts->row_end - opts->row_begin;
     const uint32_t band = opts->band_rows ? opts->band_rows : std::max(1u, rows);
     v.row0 = opts->row_begin;

@@ -57,14 +57,19 @@ struct KView {
     uint32_t row0, band_rows, rank, nranks, local_rows, row_limit;
     uint32_t* out;
     unsigned long long* bytes;
-    uint32_t* defer;          // crawl deferral slot: [count, done, entries (l << 16 | x)...]
+    uint32_t* defer;          // crawl deferral slot: [count, done, 0, 0, records (kDeferRecWords each)...]
     uint32_t defer_cap;
+    uint32_t crawl_rewalk;    // 1: deferred crawls are walked from the pixel's start (VR_KERNEL_TILE_REWALK)
 };
 
 // Rays that start a cluster-skip crawl (see vr_march.hip crawl_steps) in the
 // tile pass are deferred to a second pass over a per-launch list.
-constexpr uint32_t kDeferCap = 65536;
-constexpr uint32_t kDeferWords = 2 + kDeferCap;
+// A slot is [count, done, 0, 0] and kDeferCap records of kDeferRecWords words:
+// the crawling walk's state at the crawl (vr_march.hip, grid_original_rt), from
+// which the crawl pass resumes it.
+constexpr uint32_t kDeferCap = 16384;
+constexpr uint32_t kDeferRecWords = 20;
+constexpr uint32_t kDeferWords = 4 + kDeferCap * kDeferRecWords;
 
 // Launch one render (defined in vr_march.hip).
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,

@@ -105,6 +105,28 @@ __device__ __forceinline__ int32_t plane_c8(int32_t c8) {
     else return c8;
 }
 
+// A crawl iteration has t = 0, so it stepped o_i <- RN(o_i + c_i), c_i =
+// RN(EPSILON d_i); its voxel is q_i = trunc(old o_i), old o_i >= 0 (it was in
+// the region).  The old coordinate lies within ulp(on)/2 + ulp(e)/2 of
+// e = RN(on - c) (< 1.5 ulp(e) for e >= 1), so it is one of the floats at most 4
+// steps from e that step to `on`: q is found when all of those truncate alike.
+__device__ __forceinline__ bool crawl_voxel(float on, float c, int32_t& q) {
+    const float e = on - c;
+    if (e + 0x1p-20f < 1.0f) { q = 0; return true; }          // every candidate in [0, 1)
+    int32_t found = -1;
+    bool ok = true;
+#pragma unroll 1
+    for (int32_t k = -4; k <= 4; ++k) {
+        const float x = __uint_as_float(__float_as_uint(e) + (uint32_t)k);
+        if (!(x >= 0.0f) || x + c != on) continue;
+        const int32_t t = f2i(x);
+        ok &= found < 0 || t == found;
+        found = t;
+    }
+    q = found;
+    return ok && found >= 0;
+}
+
 // CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
 // crawling ray reserves an entry in the launch's deferral list and unwinds.
 template <int STORE, bool COUNT, bool CRAWL>
@@ -114,6 +136,9 @@ struct Walker : Ctx<STORE, COUNT> {
     using C::lighting; using C::normal_from_t; using C::in_region; using C::grid_in_region;
     using C::advance_region; using C::in_scene; using C::region_at; using C::skip_null; using C::bytes;
     __device__ Walker(const KScene& s_, const KView& v_) : C(s_, v_) {}
+    // what a deferred crawl must know to be resumed (see the deferral below):
+    // bit 1 = the shadow walk is the longest-axis one; the lit colour of the hit
+    uint32_t ctx = 0, lit_saved = 0;
 
     // rayMarchVoxelGrid (Renderer.cuh:260-336) and, SHADOW, shadowRayMarchVoxelGrid (:100-172).
     // The cluster-skip step (:290-306) and the voxel step (:318-331) share one
@@ -130,23 +155,32 @@ struct Walker : Ctx<STORE, COUNT> {
     // one division per iteration instead of three, and (t + EPSILON) * d_i is
     // one product.  Bit-identical; shadow walks read no per-axis t values.
     template <bool SHADOW, bool EQ = false>
-    __device__ __forceinline__ bool grid_original(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h) {
-        return grid_original_rt(o, d, reg, cr, h, SHADOW, SHADOW && EQ);
+    __device__ __forceinline__ bool grid_original(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h,
+                                                  const uint32_t* rs = nullptr) {
+        return grid_original_rt(o, d, reg, cr, h, SHADOW, SHADOW && EQ, rs);
     }
     // The same with the shadow flag a per-lane value (fused primary + shadow
     // walk); the template form above constant-folds it.
+    // rs (crawl pass only): a deferral record -- resume the walk at its crawl.
     __device__ __forceinline__ bool grid_original_rt(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h, const bool SHADOW,
-                                                     const bool EQ) {
+                                                     const bool EQ, const uint32_t* rs = nullptr) {
+        const bool resume = CRAWL && rs != nullptr;
         const bool px = d.x > 0.0f, py = d.y > 0.0f, pz = d.z > 0.0f;
         const bool zx = SHADOW && d.x == 0.0f, zy = SHADOW && d.y == 0.0f, zz = SHADOW && d.z == 0.0f;
         float nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
         float nY = py ? ceilf(o.y) + kEps : floorf(o.y) - kEps;
         float nZ = pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps;
-        float tX = zx ? kInf : (nX - o.x) / d.x;
-        float tY = zy ? kInf : (nY - o.y) / d.y;
-        float tZ = zz ? kInf : (nZ - o.z) / d.z;
-        float tMin = fminf(tX, fminf(tY, tZ));
-        o = add(o, scl(tMin + kEps, d));
+        float tX, tY, tZ, tMin;
+        if (resume) {                             // o is the stepped position of the crawl
+            tX = __uint_as_float(rs[11]); tY = __uint_as_float(rs[12]);
+            tZ = __uint_as_float(rs[13]); tMin = __uint_as_float(rs[14]);
+        } else {
+            tX = zx ? kInf : (nX - o.x) / d.x;
+            tY = zy ? kInf : (nY - o.y) / d.y;
+            tZ = zz ? kInf : (nZ - o.z) / d.z;
+            tMin = fminf(tX, fminf(tY, tZ));
+            o = add(o, scl(tMin + kEps, d));
+        }
         uint32_t col = kEmpty;
         if constexpr (STORE == STORE_VCS) {
             // Inside the region every voxel coordinate is in [0, 64): the mask
@@ -167,9 +201,10 @@ struct Walker : Ctx<STORE, COUNT> {
             uint32_t crawl_after = 0;
             bool crawl_off = false;
             uint32_t vi = 0;
-            int32_t qx = 0, qy = 0, qz = 0;   // voxel of the iteration that exited to crawl
+            int32_t qx = 0, qy = 0, qz = 0;   // crawl pass: voxel of the iteration that exited to crawl
             Blk blk{0u, kNone};
             uint32_t bit = 0;
+            bool resume_now = resume;
             for (;;) {
                 // Per-walk constants, (re)made here in the crawl pass so they are
                 // dead across the crawl code below (the barrier keeps them from
@@ -187,95 +222,105 @@ struct Walker : Ctx<STORE, COUNT> {
                 // one compare per iteration: min |n| >= lim (lim = +inf sends the lane
                 // to the slow branch every iteration; |n| < 73 inside a region)
                 const float nlim = walk_ok ? 0x1p-90f : kInf;
-                // The loop, specialised for a wave whose lanes share the signs of the
-                // direction (nearly every primary tile; every shadow walk): the planes
-                // then need no sign multiplications (see plane_v / plane_c8).
-                auto walk = [&](auto SXc, auto SYc, auto SZc) {
-                    constexpr int SX = decltype(SXc)::value, SY = decltype(SYc)::value, SZ = decltype(SZc)::value;
-                    for (;;) {
-                        ++this->iters;
-                        const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-                        this->count(4);
-                        const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
-                        blk = mreg[wi];
-                        // both candidate planes, computed while the mask word is in
-                        // flight and materialised (with the whole 8-B word: one load)
-                        float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey), vZ = plane_v<SZ>(o.z, gz, ez);
-                        // (in the region v < 64, so v & ~7 == v & 0x38, the form word_index shares)
-                        float cX = (float)((vx & 0x38) + plane_c8<SX>(cx8)), cY = (float)((vy & 0x38) + plane_c8<SY>(cy8)),
-                              cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
-                        asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
-                        const bool skip = absent(blk);
-                        bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
-                        // 0 or ~0 (an absent cluster's words have no bits set)
-                        const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)blk.x, bit, 1u);
-                        found = fm != 0u;
-                        vi = blk.y + __popc(blk.x & ((1u << (bit & 31u)) - 1u));
-                        if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
-                        nX = skip ? cX : vX;
-                        nY = skip ? cY : vY;
-                        nZ = skip ? cZ : vZ;
-                        const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
-                        float sMin;
-                        crawl = false;
-                        if (EQ) {
-                            // |a_i| / |d| = a_i / d up to the sign of a zero (t = -0 for
-                            // a = +0, d < 0), which neither the step nor the crawl test sees
-                            const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
-                            sMin = div_fast(am, rx);
-                            const bool bad = !(am >= nlim);
-                            if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                                sMin = bad ? am / fabsf(d.x) : sMin;
-                                crawl = bad & walk_ok & skip & (sMin == 0.0f) &
-                                        (CRAWL ? this->iters >= crawl_after : !crawl_off);
-                            }
-                        } else {
-                            float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
-                            const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
-                            if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                                sX = bad ? (zx ? kInf : ax / d.x) : sX;
-                                sY = bad ? (zy ? kInf : ay / d.y) : sY;
-                                sZ = bad ? (zz ? kInf : az / d.z) : sZ;
-                                // a skip step with t = 0 (its plane axis has n = 0, so it is
-                                // always on this branch): the ray creeps through an empty cluster
-                                crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
-                                        (CRAWL ? this->iters >= crawl_after : !crawl_off);
-                            }
-                            sMin = fminf(sX, fminf(sY, sZ));
-                            const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
-                            tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
-                        }
-                        const f3 on = EQ ? add(o, f3{(sMin + kEps) * d.x, (sMin + kEps) * d.x, (sMin + kEps) * d.x})
-                                         : add(o, scl(sMin + kEps, d));
-                        qx = vx; qy = vy; qz = vz;
-                        // a hit keeps o unstepped (bit-select on the hit mask)
-                        o.x = bit_select(fm, o.x, on.x);
-                        o.y = bit_select(fm, o.y, on.y);
-                        o.z = bit_select(fm, o.z, on.z);
-                        // One unsigned compare for hit, region exit (in_region_bits_nz of the
-                        // stepped position) and the budget (iters >= kIterBudget):
-                        const uint32_t ev = max(max(max(max(__float_as_uint(on.x), __float_as_uint(on.y)), __float_as_uint(on.z)),
-                                                    this->iters + (0x42800000u - kIterBudget)), fm);
-                        if (ev >= 0x42800000u || crawl) break;
-                    }
-                };
-                const uint32_t sg = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
-                const uint32_t sg0 = __builtin_amdgcn_readfirstlane(sg);
-                using N = Sgn<-1>;
-                using P = Sgn<1>;
-                if (!CRAWL && __builtin_amdgcn_ballot_w64(sg != sg0) == 0 && (!EQ || sg0 == 0u || sg0 == 7u)) {
-                    switch (sg0) {
-                    case 0: walk(N{}, N{}, N{}); break;
-                    case 7: walk(P{}, P{}, P{}); break;
-                    case 1: if (!EQ) walk(P{}, N{}, N{}); break;
-                    case 2: if (!EQ) walk(N{}, P{}, N{}); break;
-                    case 3: if (!EQ) walk(P{}, P{}, N{}); break;
-                    case 4: if (!EQ) walk(N{}, N{}, P{}); break;
-                    case 5: if (!EQ) walk(P{}, N{}, P{}); break;
-                    default: if (!EQ) walk(N{}, P{}, P{}); break;
-                    }
+                if (resume_now) {
+                    // the deferred crawl: its iteration left an absent cluster (blk) at
+                    // voxel q with o stepped; the post-loop test below re-finds the crawl
+                    resume_now = false;
+                    blk = Blk{0u, kNone};
+                    bit = 0;
+                    qx = (int32_t)rs[15]; qy = (int32_t)rs[16]; qz = (int32_t)rs[17];
                 } else {
-                    walk(Sgn<0>{}, Sgn<0>{}, Sgn<0>{});
+                    // The loop, specialised for a wave whose lanes share the signs of the
+                    // direction (nearly every primary tile; every shadow walk): the planes
+                    // then need no sign multiplications (see plane_v / plane_c8).
+                    auto walk = [&](auto SXc, auto SYc, auto SZc) {
+                        constexpr int SX = decltype(SXc)::value, SY = decltype(SYc)::value, SZ = decltype(SZc)::value;
+                        for (;;) {
+                            ++this->iters;
+                            const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
+                            this->count(4);
+                            const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
+                            blk = mreg[wi];
+                            // both candidate planes, computed while the mask word is in
+                            // flight and materialised (with the whole 8-B word: one load)
+                            float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey), vZ = plane_v<SZ>(o.z, gz, ez);
+                            // (in the region v < 64, so v & ~7 == v & 0x38, the form word_index shares)
+                            float cX = (float)((vx & 0x38) + plane_c8<SX>(cx8)), cY = (float)((vy & 0x38) + plane_c8<SY>(cy8)),
+                                  cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
+                            asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
+                            const bool skip = absent(blk);
+                            bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
+                            // 0 or ~0 (an absent cluster's words have no bits set)
+                            const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)blk.x, bit, 1u);
+                            found = fm != 0u;
+                            vi = blk.y + __popc(blk.x & ((1u << (bit & 31u)) - 1u));
+                            if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
+                            nX = skip ? cX : vX;
+                            nY = skip ? cY : vY;
+                            nZ = skip ? cZ : vZ;
+                            const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
+                            float sMin;
+                            crawl = false;
+                            if (EQ) {
+                                // |a_i| / |d| = a_i / d up to the sign of a zero (t = -0 for
+                                // a = +0, d < 0), which neither the step nor the crawl test sees
+                                const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
+                                sMin = div_fast(am, rx);
+                                const bool bad = !(am >= nlim);
+                                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                                    sMin = bad ? am / fabsf(d.x) : sMin;
+                                    crawl = bad & walk_ok & skip & (sMin == 0.0f) &
+                                            (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                                    if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
+                                }
+                            } else {
+                                float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
+                                const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
+                                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                                    sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                                    sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                                    sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                                    // a skip step with t = 0 (its plane axis has n = 0, so it is
+                                    // always on this branch): the ray creeps through an empty cluster
+                                    crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
+                                            (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                                    if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
+                                }
+                                sMin = fminf(sX, fminf(sY, sZ));
+                                const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
+                                tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
+                            }
+                            const f3 on = EQ ? add(o, f3{(sMin + kEps) * d.x, (sMin + kEps) * d.x, (sMin + kEps) * d.x})
+                                             : add(o, scl(sMin + kEps, d));
+                            // a hit keeps o unstepped (bit-select on the hit mask)
+                            o.x = bit_select(fm, o.x, on.x);
+                            o.y = bit_select(fm, o.y, on.y);
+                            o.z = bit_select(fm, o.z, on.z);
+                            // One unsigned compare for hit, region exit (in_region_bits_nz of the
+                            // stepped position) and the budget (iters >= kIterBudget):
+                            const uint32_t ev = max(max(max(max(__float_as_uint(on.x), __float_as_uint(on.y)), __float_as_uint(on.z)),
+                                                        this->iters + (0x42800000u - kIterBudget)), fm);
+                            if (ev >= 0x42800000u || crawl) break;
+                        }
+                    };
+                    const uint32_t sg = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
+                    const uint32_t sg0 = __builtin_amdgcn_readfirstlane(sg);
+                    using N = Sgn<-1>;
+                    using P = Sgn<1>;
+                    if (!CRAWL && __builtin_amdgcn_ballot_w64(sg != sg0) == 0 && (!EQ || sg0 == 0u || sg0 == 7u)) {
+                        switch (sg0) {
+                        case 0: walk(N{}, N{}, N{}); break;
+                        case 7: walk(P{}, P{}, P{}); break;
+                        case 1: if (!EQ) walk(P{}, N{}, N{}); break;
+                        case 2: if (!EQ) walk(N{}, P{}, N{}); break;
+                        case 3: if (!EQ) walk(P{}, P{}, N{}); break;
+                        case 4: if (!EQ) walk(N{}, N{}, P{}); break;
+                        case 5: if (!EQ) walk(P{}, N{}, P{}); break;
+                        default: if (!EQ) walk(N{}, P{}, P{}); break;
+                        }
+                    } else {
+                        walk(Sgn<0>{}, Sgn<0>{}, Sgn<0>{});
+                    }
                 }
                 // Why the lane left, recomputed from values the loop keeps in VGPRs
                 // anyway (a flag read after a divergent loop is carried through it as
@@ -305,7 +350,31 @@ struct Walker : Ctx<STORE, COUNT> {
                             const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
                             const uint32_t px_ = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
                             const uint32_t pl_ = (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
-                            v.defer[2 + idx] = (pl_ << 16) | px_;
+                            uint32_t* r = v.defer + 4 + (size_t)idx * kDeferRecWords;
+                            r[0] = (pl_ << 16) | px_;
+                            r[1] = (SHADOW ? 1u : 0u) | this->ctx;
+                            r[2] = __float_as_uint(o.x); r[3] = __float_as_uint(o.y); r[4] = __float_as_uint(o.z);
+                            r[5] = (uint32_t)cr.x; r[6] = (uint32_t)cr.y; r[7] = (uint32_t)cr.z;
+                            r[8] = 0u;                                  // (the crawl pass reads it again)
+                            r[9] = this->iters;
+                            r[10] = this->bytes;
+                            // (a shadow walk has no normal: its t values are not kept live for this)
+                            r[11] = SHADOW ? 0u : __float_as_uint(tX); r[12] = SHADOW ? 0u : __float_as_uint(tY);
+                            r[13] = SHADOW ? 0u : __float_as_uint(tZ); r[14] = SHADOW ? 0u : __float_as_uint(tMin);
+                            // The crawl iteration's voxel q (see crawl_voxel): recovered from
+                            // the stepped position; if it cannot be, the crawl pass walks the
+                            // pixel from its start instead.
+                            bool amb = false;
+                            uint32_t qq[3];
+#pragma unroll 1
+                            for (uint32_t a = 0; a < 3u; ++a) {
+                                int32_t qa;
+                                amb |= !crawl_voxel(comp(o, a), kEps * comp(d, a), qa);
+                                qq[a] = (uint32_t)qa;
+                            }
+                            r[1] |= (amb || v.crawl_rewalk) ? 4u : 0u;
+                            r[15] = qq[0]; r[16] = qq[1]; r[17] = qq[2];
+                            r[18] = this->lit_saved;
                             if (COUNT) this->bytes = 0xFFFFFFFCu;     // + the final 4 = 0
                             aborted = true;
                             return false;
@@ -766,6 +835,18 @@ struct Walker : Ctx<STORE, COUNT> {
             cr = i3{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
         }
         f3 o = sub(so, mk((float)(cr.x * kBlock), (float)(cr.y * kBlock), (float)(cr.z * kBlock)));
+        return primary_regions<ALGO>(o, d, cr, h, nullptr);
+    }
+    // The region walk of rayMarchVoxelScene(LongestAxis) (:376-433); rs (crawl
+    // pass): first finish the region walk a deferral record left at its crawl.
+    template <int ALGO>
+    __device__ __forceinline__ bool primary_regions(f3 o, f3 d, i3 cr, Hit& h, const uint32_t* rs) {
+        if (CRAWL && rs != nullptr) {
+            const bool hit = grid_original_rt(o, d, this->region_at_nocount(cr), cr, h, false, false, rs);
+            if (aborted) return false;
+            if (hit) return true;
+            advance_region(cr, o);
+        }
         while (in_scene(cr)) {
             if (!tick()) return false;
             uint32_t reg = region_at(cr);
@@ -786,9 +867,15 @@ struct Walker : Ctx<STORE, COUNT> {
     // isInShadowOriginalRayMarch (Renderer.cuh:174-235) /
     // isInShadowRayMarchVoxelSceneLongestAxis (:633-694).
     template <bool LONGEST, bool EQ = false>
-    __device__ __forceinline__ bool shadow(f3 o, i3 cr) {
+    __device__ __forceinline__ bool shadow(f3 o, i3 cr, const uint32_t* rs = nullptr) {
         f3 d = ld3(v.L);
         Hit dummy;
+        if (CRAWL && rs != nullptr) {            // resume a deferred crawl (as primary_regions)
+            const bool hit = grid_original_rt(o, d, this->region_at_nocount(cr), cr, dummy, true, EQ, rs);
+            if (aborted) return false;
+            if (hit) return true;
+            advance_region(cr, o);
+        }
         while (in_scene(cr)) {
             if (!tick()) return false;
             uint32_t reg = region_at(cr);
@@ -807,40 +894,87 @@ struct Walker : Ctx<STORE, COUNT> {
     }
 };
 
+// calculateWorldRay (Renderer.cuh:1013-1022) + Camera::generateRay (Camera.cuh:25-29)
+// for pixel (x, local row l); false when the row is outside the frame.
+__device__ __forceinline__ bool pixel_ray(const KView& v, uint32_t x, uint32_t l, f3& ro, f3& rd) {
+    const uint32_t band = l / v.band_rows;
+    const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
+    if (y >= v.row_limit) return false;
+    float u = ((float)x + 0.5f) / (float)v.W;
+    float vv = ((float)(v.H - y) + 0.5f) / (float)v.H;
+    ro = add(add(ld3(v.llc), scl(u, ld3(v.hor))), scl(vv, ld3(v.ver)));
+    rd = unit(sub(ro, ld3(v.org)));
+    return true;
+}
+
+// applyLighting at the primary hit (Renderer.cuh:249-258; regionWorldPosition :413)
+// times !shadow (:315,737,821): the pixel's colour.
+template <int STORE, bool COUNT, bool CRAWL>
+__device__ __forceinline__ uint32_t light_and_shadow(Walker<STORE, COUNT, CRAWL>& w, const KView& v, const Hit& h) {
+    bool sh = false;
+    const f3 rwp = add(ld3(v.translation), mk((float)(h.region.x * kBlock), (float)(h.region.y * kBlock),
+                                              (float)(h.region.z * kBlock)));
+    const uint32_t lit = w.lighting(h.col, h.n, rwp, h.so);
+    if (v.use_shadows) {
+        w.lit_saved = lit;
+        const bool eq = v.L[0] == v.L[1] && v.L[1] == v.L[2];
+        if (h.longest) {
+            w.ctx = 2u;
+            sh = w.template shadow<true>(h.so, h.region);
+        } else {
+            sh = eq ? w.template shadow<false, true>(h.so, h.region) : w.template shadow<false>(h.so, h.region);
+        }
+    }
+    return lit * (uint32_t)!sh;
+}
+
 // The body of rayMarchSceneOriginal / rayMarchSceneJumpAxis (Renderer.cuh:1033-1063)
 // for pixel (x, local row l): colour, algorithmic bytes (+4 for the pixel write)
 // (a pixel deferred to the crawl pass comes back as 0 with 0 bytes).
 template <int STORE, int ALGO, bool COUNT, bool CRAWL>
 __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, const float* inv255, uint32_t x, uint32_t l,
                                           uint32_t& bytes) {
-    const uint32_t band = l / v.band_rows;
-    const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
     uint32_t col = 0;
     bytes = 0;
-    if (y < v.row_limit) {
-        // calculateWorldRay (Renderer.cuh:1013-1022) + Camera::generateRay (Camera.cuh:25-29)
-        float u = ((float)x + 0.5f) / (float)v.W;
-        float vv = ((float)(v.H - y) + 0.5f) / (float)v.H;
-        f3 ro = add(add(ld3(v.llc), scl(u, ld3(v.hor))), scl(vv, ld3(v.ver)));
-        f3 rd = unit(sub(ro, ld3(v.org)));
+    f3 ro, rd;
+    if (pixel_ray(v, x, l, ro, rd)) {
         Walker<STORE, COUNT, CRAWL> w(s, v);
         w.inv255 = inv255;
         Hit h;
-        if (w.template primary<ALGO>(ro, rd, h)) {
-            bool sh = false;
-            // applyLighting (Renderer.cuh:249-258) at the hit; regionWorldPosition (:413)
-            const f3 rwp = add(ld3(v.translation), mk((float)(h.region.x * kBlock), (float)(h.region.y * kBlock),
-                                                      (float)(h.region.z * kBlock)));
-            const uint32_t lit = w.lighting(h.col, h.n, rwp, h.so);
-            if (v.use_shadows)
-                sh = h.longest ? w.template shadow<true>(h.so, h.region)
-                     : v.L[0] == v.L[1] && v.L[1] == v.L[2] ? w.template shadow<false, true>(h.so, h.region)
-                                                            : w.template shadow<false>(h.so, h.region);
-            col = lit * (uint32_t)!sh;
-        }
+        if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
         if (w.aborted) col = 0;
         bytes = w.bytes + 4u;                     // + the pixel write
     }
+    return col;
+}
+
+// The crawl pass's pixel: the walk a deferral record `r` left at its crawl,
+// finished from there (its iterations and bytes so far are the record's).
+template <int STORE, int ALGO, bool COUNT>
+__device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v, const float* inv255,
+                                                 const uint32_t* r, uint32_t& bytes) {
+    const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
+    Walker<STORE, COUNT, true> w(s, v);
+    w.inv255 = inv255;
+    w.iters = r[9];
+    w.bytes = r[10];
+    const f3 o{__uint_as_float(r[2]), __uint_as_float(r[3]), __uint_as_float(r[4])};
+    const i3 cr{(int32_t)r[5], (int32_t)r[6], (int32_t)r[7]};
+    uint32_t col = 0;
+    if (!(r[1] & 1u)) {                           // the primary walk crawled
+        f3 ro, rd;
+        pixel_ray(v, x, l, ro, rd);
+        Hit h;
+        if (w.template primary_regions<ALGO>(o, rd, cr, h, r)) col = light_and_shadow(w, v, h);
+    } else {                                      // the shadow walk crawled
+        const bool eq = v.L[0] == v.L[1] && v.L[1] == v.L[2];
+        bool sh;
+        if (r[1] & 2u) sh = eq ? w.template shadow<true, true>(o, cr, r) : w.template shadow<true>(o, cr, r);
+        else sh = eq ? w.template shadow<false, true>(o, cr, r) : w.template shadow<false>(o, cr, r);
+        col = r[18] * (uint32_t)!sh;
+    }
+    if (w.aborted) col = 0;
+    bytes = w.bytes + 4u;
     return col;
 }
 
@@ -884,9 +1018,12 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     const float* inv255 = load_inv255(inv255_lds);
     unsigned long long bytes = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t e = v.defer[2 + i], x = e & 0xFFFFu, l = e >> 16;
+        const uint32_t* r = v.defer + 4 + (size_t)i * kDeferRecWords;
         uint32_t b;
-        v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, true>(s, v, inv255, x, l, b);
+        const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
+        // an ambiguous crawl voxel (see the deferral): walk the pixel from its start
+        v.out[(size_t)l * v.W + x] = (r[1] & 4u) ? shade<STORE, ALGO, COUNT, true>(s, v, inv255, x, l, b)
+                                                 : shade_resume<STORE, ALGO, COUNT>(s, v, inv255, r, b);
         bytes += b;
     }
     if (COUNT) add_bytes(v, threadIdx.x & 63u, bytes);

@@ -260,6 +260,7 @@ class Kernel(enum.IntEnum):
     AUTO = _capi.VR_KERNEL_AUTO
     TILE = _capi.VR_KERNEL_TILE
     PERSISTENT = _capi.VR_KERNEL_PERSISTENT
+    TILE_REWALK = _capi.VR_KERNEL_TILE_REWALK
 
 
 def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
