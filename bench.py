@@ -9,7 +9,7 @@ A step = one full frame.  N = 1: the C2 frame exactly.  N > 1 (one rank per
 GPU, torch.distributed.run, RCCL): weak scaling over image tiles -- the same
 view at N x the pixels (each side x sqrt(N), ~1920x1080 per GPU), rows split
 into interleaved 8-row bands (band b -> rank b % N), and every frame gathered
-to rank 0 over RCCL and assembled there.  Two frames are in flight
+to rank 0 over RCCL as RGB8 (3 B per pixel) and assembled there.  Two frames are in flight
 (tiles.BandGather: two band buffers, each with its own stream): the long waves
 that end frame k overlap the start of frame k+1, and frame k's gather runs beside
 frame k+1's render.  Every frame is still rendered in full.  Inputs (scene,
@@ -111,7 +111,9 @@ def main():
     lit = vr.setup_constant_values()
     info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
     stream = torch.cuda.current_stream()
-    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=args.frames_in_flight)
+    # N > 1: bands travel as the RGB8 framebuffer (writeColorToFramebuffer's format, 3 B per
+    # pixel): rank 0 ends each frame with the RGB8 image
+    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=args.frames_in_flight, rgb8=world > 1)
 
     def render(buf):   # on the current stream (BandGather's slot stream in the loops)
         vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, rank, world, buf)
@@ -205,7 +207,8 @@ def main():
                        "grid": cfg.grid, "width": W, "height": H,
                        "store": cfg.store.name, "algorithm": cfg.algorithm.name, "scale": cfg.scale,
                        "voxels": int(len(rgb)), "parallelism": f"row-band tiles x{world}" +
-                       (" + RCCL gather to rank 0 (overlapped with the next frame)" if world > 1 else ""),
+                       (" + RCCL gather of the RGB8 bands to rank 0 (overlapped with the next frame)"
+                        if world > 1 else ""),
                        "frames_in_flight": pipe.depth},
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_median": round(kern_median, 4),

@@ -9,6 +9,7 @@ from __future__ import annotations
 import pytest
 import torch
 
+import voxelraymarcher_amd as vr
 from voxelraymarcher_amd import tiles
 from voxelraymarcher_amd.tiles import BandGather, owned_rows
 
@@ -23,7 +24,8 @@ class _Work:
         torch.cuda.current_stream().wait_event(self.ev)
 
 
-def test_band_gather_rank0_side_stream(monkeypatch):
+@pytest.mark.parametrize("rgb8", [False, True], ids=["words", "rgb8"])
+def test_band_gather_rank0_side_stream(monkeypatch, rgb8):
     W, H, B, R, frames = 64, 77, 8, 3, 9
     dev = torch.device("cuda", 0)
 
@@ -31,11 +33,12 @@ def test_band_gather_rank0_side_stream(monkeypatch):
         return ((torch.arange(W * H, dtype=torch.int64, device=dev) * 2654435761 + 977 * k) % (1 << 24)) \
             .to(torch.int32).reshape(H, W)
 
-    def rank_buffer(k, r, words):
+    def rank_buffer(k, r, n):
+        words = n // 3 if rgb8 else n
         buf = torch.zeros(words, dtype=torch.int32, device=dev)
         rows = owned_rows(H, B, r, R)
         buf.view(-1, W)[:len(rows)] = expected(k)[torch.tensor(rows, device=dev)]
-        return buf
+        return vr.pack_rgb8(buf) if rgb8 else buf
 
     gstream = torch.cuda.Stream(dev)
     kbox = [0]
@@ -59,7 +62,7 @@ def test_band_gather_rank0_side_stream(monkeypatch):
     import torch.distributed as dist
     monkeypatch.setattr(dist, "gather", fake_gather)
     got = []
-    pipe = BandGather(W, H, B, 0, R, dev, depth=2, on_frame=lambda f: got.append(f.clone()))
+    pipe = BandGather(W, H, B, 0, R, dev, depth=2, on_frame=lambda f: got.append(f.clone()), rgb8=rgb8)
     assert pipe.side is not None
 
     def render(buf):
@@ -76,5 +79,6 @@ def test_band_gather_rank0_side_stream(monkeypatch):
     assert sent == list(range(frames))
     assert len(got) == frames
     for k, g in enumerate(got):
-        assert torch.equal(g, expected(k)), f"frame {k} differs"
+        want = vr.pack_rgb8(expected(k).reshape(-1)).view(H, W, 3) if rgb8 else expected(k)
+        assert torch.equal(g, want), f"frame {k} differs"
     assert tiles is not None

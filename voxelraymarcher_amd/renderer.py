@@ -326,9 +326,12 @@ def render_bands(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camer
     return out
 
 
-def pack_rgb8(words: torch.Tensor, stream=None) -> torch.Tensor:
-    """writeColorToFramebuffer (Renderer.cuh:1024-1031) on the device: words -> RGB8 bytes."""
-    rgb = torch.empty(words.numel() * 3, dtype=torch.uint8, device=words.device)
+def pack_rgb8(words: torch.Tensor, stream=None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """writeColorToFramebuffer (Renderer.cuh:1024-1031) on the device: words -> RGB8 bytes
+    (into `out`, uint8 of 3 x words.numel(), when given)."""
+    rgb = torch.empty(words.numel() * 3, dtype=torch.uint8, device=words.device) if out is None else out
+    if rgb.dtype != torch.uint8 or rgb.numel() != words.numel() * 3 or not rgb.is_contiguous():
+        raise ValueError("out must be a contiguous uint8 tensor of 3 x words.numel() bytes")
     check(lib().vr_pack_rgb8(c_void_p(words.data_ptr()), c_void_p(rgb.data_ptr()), words.numel(),
                              _stream_ptr(stream)), "vr_pack_rgb8")
     return rgb

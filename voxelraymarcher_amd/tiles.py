@@ -63,15 +63,23 @@ class BandGather:
     """
 
     def __init__(self, width: int, height: int, band_rows: int, rank: int, nranks: int,
-                 device, depth: int = 2, on_frame=None):
+                 device, depth: int = 2, on_frame=None, rgb8: bool = False):
         self.W, self.H, self.B = width, height, band_rows
         self.rank, self.R, self.depth = rank, nranks, depth
         words = band_buffer_words(width, height, band_rows, nranks)
         self.per = bands_per_rank(height, band_rows, nranks)
         self.bufs = [torch.empty(words, dtype=torch.int32, device=device) for _ in range(depth)]
-        self.recv = ([torch.empty((nranks, words), dtype=torch.int32, device=device) for _ in range(depth)]
+        # rgb8 (GPUs, N > 1): the bands travel as the RGB8 framebuffer (3 B per pixel
+        # instead of the 4-B packed word: a quarter less over xGMI) and rank 0
+        # assembles an RGB8 frame [H, W, 3]
+        self.rgb8 = bool(rgb8) and nranks > 1
+        self.px = 3 if self.rgb8 else 1                  # elements per pixel in the exchanged buffers
+        xdt = torch.uint8 if self.rgb8 else torch.int32
+        self.packed = ([torch.empty(words * 3, dtype=torch.uint8, device=device) for _ in range(depth)]
+                       if self.rgb8 else None)
+        self.recv = ([torch.empty((nranks, words * self.px), dtype=xdt, device=device) for _ in range(depth)]
                      if (rank == 0 and nranks > 1) else None)
-        self.frame = (torch.empty((self.per * nranks * band_rows, width), dtype=torch.int32, device=device)
+        self.frame = (torch.empty((self.per * nranks * band_rows, width * self.px), dtype=xdt, device=device)
                       if rank == 0 else None)
         self.work = [None] * depth
         dev = torch.device(device)
@@ -90,10 +98,12 @@ class BandGather:
         return torch.cuda.stream(self.streams[slot]) if self.streams is not None else contextlib.nullcontext()
 
     def _assemble(self, slot: int) -> None:
-        src = self.recv[slot].view(self.R, self.per, self.B, self.W).permute(1, 0, 2, 3)
-        self.frame.view(self.per, self.R, self.B, self.W).copy_(src)
+        rw = self.W * self.px
+        src = self.recv[slot].view(self.R, self.per, self.B, rw).permute(1, 0, 2, 3)
+        self.frame.view(self.per, self.R, self.B, rw).copy_(src)
         if self.on_frame is not None:
-            self.on_frame(self.frame[:self.H])
+            f = self.frame[:self.H]
+            self.on_frame(f.view(self.H, self.W, 3) if self.rgb8 else f)
 
     def _finish(self, slot: int) -> None:
         with self._slot_stream(slot):
@@ -127,11 +137,15 @@ class BandGather:
             render(self.bufs[slot])
             if self.R > 1:
                 import torch.distributed as dist
+                send = self.bufs[slot]
+                if self.rgb8:
+                    from .renderer import pack_rgb8
+                    send = pack_rgb8(self.bufs[slot], out=self.packed[slot])
                 dst = list(self.recv[slot].unbind(0)) if self.rank == 0 else None
                 if self.copied[slot] is not None:       # its previous frame has left recv[slot]
                     torch.cuda.current_stream().wait_event(self.copied[slot])
                     self.copied[slot] = None
-                self.work[slot] = dist.gather(self.bufs[slot], dst, dst=0, async_op=True)
+                self.work[slot] = dist.gather(send, dst, dst=0, async_op=True)
         self.pending.append(slot)
         self.k += 1
 
