@@ -2,8 +2,8 @@
 //
 // One lane per pixel; one wave64 = one 8x8 pixel tile (the reference's 8x8
 // CUDA block, Main.cu:109-111, but as a single wavefront so the tile's rays
-// walk the same clusters together); 4 waves (2x2 tiles) per 256-thread
-// workgroup.  Templated on {store, algorithm, count}: no virtual calls, no
+// walk the same clusters together), two waves (tiles side by side) per
+// 128-thread workgroup (kTilesX/kTilesY below).  Templated on {store, algorithm, count}: no virtual calls, no
 // function pointers (the reference's StorageStructure vtable,
 // StorageStructure.cuh:12-56, and nextXFunc pointers, Renderer.cuh:263-265,
 // become compile-time branches).
@@ -126,6 +126,13 @@ __device__ __forceinline__ bool crawl_voxel(float on, float c, int32_t& q) {
     q = found;
     return ok && found >= 0;
 }
+
+// Tile pass workgroup: kTilesX x kTilesY waves, one 8x8 pixel tile each.  Two
+// tiles side by side (128 threads) measured faster than 2 x 2 (256): a
+// workgroup's slot is held until its slowest wave ends, so smaller ones pack the
+// CUs more tightly (per frame in flight: C2 0.151 -> 0.1415 ms, C3 0.420 -> 0.385,
+// C4 0.101 -> 0.096; one tile per workgroup: C2 0.1423, C3 0.377, C4 0.0955).
+constexpr uint32_t kTilesX = 2, kTilesY = 1;
 
 // CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
 // crawling ray reserves an entry in the launch's deferral list and unwinds.
@@ -348,8 +355,8 @@ struct Walker : Ctx<STORE, COUNT> {
                             // (the tile pass writes this pixel as 0; the crawl pass,
                             // which runs after it, overwrites it and counts its bytes)
                             const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-                            const uint32_t px_ = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
-                            const uint32_t pl_ = (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
+                            const uint32_t px_ = (blockIdx.x * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
+                            const uint32_t pl_ = (blockIdx.y * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
                             uint32_t* r = v.defer + 4 + (size_t)idx * kDeferRecWords;
                             r[0] = (pl_ << 16) | px_;
                             r[1] = (SHADOW ? 1u : 0u) | this->ctx;
@@ -983,7 +990,7 @@ __device__ __forceinline__ void add_bytes(const KView& v, uint32_t lane, unsigne
     if (lane == 0 && b) atomicAdd(v.bytes, b);
 }
 
-// Tile pass: one lane per pixel, one wave per 8x8 tile, 2x2 tiles per workgroup.
+// Tile pass: one lane per pixel, one wave per 8x8 tile, kTilesX x kTilesY tiles per workgroup.
 #ifndef VR_ORIG_WAVES
 #define VR_ORIG_WAVES 7
 #endif
@@ -991,12 +998,12 @@ __device__ __forceinline__ void add_bytes(const KView& v, uint32_t lane, unsigne
 #define VR_LONG_WAVES 7
 #endif
 template <int STORE, int ALGO, bool COUNT>
-__global__ __launch_bounds__(256, ALGO == ALGO_ORIGINAL ? VR_ORIG_WAVES : VR_LONG_WAVES) void march_kernel(KScene s, KView v) {
+__global__ __launch_bounds__(64 * kTilesX * kTilesY, ALGO == ALGO_ORIGINAL ? VR_ORIG_WAVES : VR_LONG_WAVES) void march_kernel(KScene s, KView v) {
     __shared__ float inv255_lds[256];
     const float* inv255 = load_inv255(inv255_lds);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t x = (blockIdx.x * 2u + (wave & 1u)) * 8u + (lane & 7u);
-    const uint32_t l = (blockIdx.y * 2u + (wave >> 1)) * 8u + (lane >> 3);
+    const uint32_t x = (blockIdx.x * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
+    const uint32_t l = (blockIdx.y * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
     uint32_t bytes = 0;
     if (x < v.W && l < v.local_rows) {
         v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, false>(s, v, inv255, x, l, bytes);
@@ -1048,8 +1055,8 @@ __global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __rest
 }  // namespace
 
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream) {
-    dim3 grid((v.W + 15u) / 16u, (v.local_rows + 15u) / 16u);
-    dim3 block(256);
+    dim3 grid((v.W + 8u * kTilesX - 1u) / (8u * kTilesX), (v.local_rows + 8u * kTilesY - 1u) / (8u * kTilesY));
+    dim3 block(64u * kTilesX * kTilesY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     // VCS walks can crawl: a small crawl-pass grid follows the tile pass
     // (it exits at once when nothing was deferred).
