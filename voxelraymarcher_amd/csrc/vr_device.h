@@ -370,11 +370,20 @@ struct Ctx {
         return (R << 16) | (G << 8) | B;
     }
 
+    // copysignf(1.0f, -x), computed where it is used: the volatile barrier keeps
+    // the compiler from hoisting the three signs out of the walk loops, where they
+    // were spilled to scratch for every pixel (three VGPRs over the 7-wave budget).
+    __device__ __forceinline__ static float neg_sign_one(float x) {
+        uint32_t u = __float_as_uint(x);
+        asm volatile("" : "+v"(u));
+        return __uint_as_float((u & 0x80000000u) ^ 0xBF800000u);
+    }
+
     // getNormalFromTValues (Renderer.cuh:237-247)
     __device__ __forceinline__ static f3 normal_from_t(float tX, float tY, float tZ, float tMin, f3 d) {
-        if (tX == tMin) return mk(copysignf(1.0f, -d.x), 0.0f, 0.0f);
-        if (tY == tMin) return mk(0.0f, copysignf(1.0f, -d.y), 0.0f);
-        return mk(0.0f, 0.0f, copysignf(1.0f, -d.z));
+        if (tX == tMin) return mk(neg_sign_one(d.x), 0.0f, 0.0f);
+        if (tY == tMin) return mk(0.0f, neg_sign_one(d.y), 0.0f);
+        return mk(0.0f, 0.0f, neg_sign_one(d.z));
     }
 
     __device__ __forceinline__ static bool in_region(f3 o) {               // Renderer.cuh:93-98
