@@ -995,7 +995,7 @@ __device__ __forceinline__ void add_bytes(const KView& v, uint32_t lane, unsigne
 #define VR_ORIG_WAVES 7
 #endif
 #ifndef VR_LONG_WAVES
-#define VR_LONG_WAVES 7
+#define VR_LONG_WAVES 6
 #endif
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(64 * kTilesX * kTilesY, ALGO == ALGO_ORIGINAL ? VR_ORIG_WAVES : VR_LONG_WAVES) void march_kernel(KScene s, KView v) {
