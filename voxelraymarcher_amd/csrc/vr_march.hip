@@ -295,7 +295,7 @@ struct Walker : Ctx<STORE, COUNT> {
                                 }
                                 sMin = fminf(sX, fminf(sY, sZ));
                                 const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
-                                tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ; tMin = vox ? sMin : tMin;
+                                tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ;   // (tMin: min of the three, at the use)
                             }
                             const f3 on = EQ ? add(o, f3{(sMin + kEps) * d.x, (sMin + kEps) * d.x, (sMin + kEps) * d.x})
                                              : add(o, scl(sMin + kEps, d));
@@ -367,7 +367,7 @@ struct Walker : Ctx<STORE, COUNT> {
                             r[10] = this->bytes;
                             // (a shadow walk has no normal: its t values are not kept live for this)
                             r[11] = SHADOW ? 0u : __float_as_uint(tX); r[12] = SHADOW ? 0u : __float_as_uint(tY);
-                            r[13] = SHADOW ? 0u : __float_as_uint(tZ); r[14] = SHADOW ? 0u : __float_as_uint(tMin);
+                            r[13] = SHADOW ? 0u : __float_as_uint(tZ); r[14] = SHADOW ? 0u : __float_as_uint(fminf(tX, fminf(tY, tZ)));
                             // The crawl iteration's voxel q (see crawl_voxel): recovered from
                             // the stepped position; if it cannot be, the crawl pass walks the
                             // pixel from its start instead.
@@ -467,7 +467,7 @@ struct Walker : Ctx<STORE, COUNT> {
                 this->count(m1 ? 8u : (m2 ? 12u : 8u));
                 const uint32_t fm = (m1 | m2) ? ~0u : 0u;
                 if (!SHADOW && !EQ) {                     // a non-hit step: its t values feed the normal
-                    tX = fm ? tX : sX; tY = fm ? tY : sY; tZ = fm ? tZ : sZ; tMin = fm ? tMin : sMin;
+                    tX = fm ? tX : sX; tY = fm ? tY : sY; tZ = fm ? tZ : sZ;
                 }
                 o.x = bit_select(fm, o.x, on.x);
                 o.y = bit_select(fm, o.y, on.y);
@@ -488,7 +488,9 @@ struct Walker : Ctx<STORE, COUNT> {
         if (col == kEmpty) return false;
         if (!SHADOW) {
             h.col = col;
-            h.n = normal_from_t(tX, tY, tZ, tMin, d);
+            // tMin is always min(tX, tY, tZ) of the same step: recomputed here
+            // instead of carried through the loop
+            h.n = normal_from_t(tX, tY, tZ, fminf(tX, fminf(tY, tZ)), d);
             h.so = o;
             h.region = cr;
             h.longest = false;
