@@ -19,7 +19,11 @@ the last frame's gather and assembly.  Rank 0 prints ONE JSON line.
 `value`/`ms_per_step` are the pipelined throughput; `kernel_ms` is one launch
 timed alone (HIP events, nothing overlapping).  roofline.achieved = the
 algorithmic bytes of one launch x launches per second in the
-timed loop; `achieved_isolated` uses `kernel_ms` instead.
+timed loop; `achieved_isolated` uses `kernel_ms` instead.  The scene is
+L2/MALL-resident, so those bytes are mostly served on-die: the roofline also
+carries the PMC-measured HBM bytes (traffic, hbm_measured_*) and the VALU-issue
+fraction that actually bounds the walk (valu_issue_frac), both from the
+round's profile (profiles/traffic.json, written by profiles/collect_traffic.py).
 """
 from __future__ import annotations
 
@@ -181,14 +185,39 @@ def main():
     if rank == 0:
         achieved = launch_bytes / (ms_per_step * 1e-3) / 1e9          # launches overlap: per-launch throughput
         achieved_isolated = launch_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, tj = None, {}
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if tj.get("config") == cfg.name and tj.get("world") == world:
                 traffic = tj.get("hbm_bytes_per_launch")
+            else:
+                tj = {}
         except (OSError, ValueError):
             pass
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "achieved_basis": "algorithmic bytes per launch (SURVEY 8(d): the words the reference walk reads, "
+                                  "counted by the instrumented kernel) / time per launch",
+                "achieved_isolated": round(achieved_isolated, 1),
+                "frac_isolated": round(achieved_isolated / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes_per_launch": launch_bytes, "algorithmic_bytes_per_frame": frame_bytes}
+        if traffic:
+            # what HBM actually serves: the scene is L2/MALL-resident, so the measured
+            # DRAM bytes (PMC, profiles/) are a small fraction of the algorithmic ones
+            hbm = traffic / (ms_per_step * 1e-3) / 1e9
+            roof.update({"hbm_measured_gbs": round(hbm, 1), "hbm_measured_frac": round(hbm / HBM_PEAK_GBS, 4),
+                         "algorithmic_over_hbm_bytes": round(launch_bytes / traffic, 1)})
+        if tj.get("valu_insts_per_launch") and tj.get("grbm_gui_active_per_launch") and tj.get("rocprof_avg_ns"):
+            # the limiter: VALU issue of the dependent walk (2 cycles per wave64
+            # instruction on each of the 1024 SIMD-32s) at the clock the profile measured
+            cyc = tj["grbm_gui_active_per_launch"] / 8.0                 # GRBM sums the 8 XCDs
+            ghz = cyc / tj["rocprof_avg_ns"]
+            valu_cyc = 2.0 * tj["valu_insts_per_launch"]
+            roof["limiter"] = "VALU issue and memory latency of the per-pixel walk (not HBM bandwidth)"
+            roof["valu_issue_frac"] = round(valu_cyc / (1024 * ghz * ms_per_step * 1e6), 4)
+            roof["valu_issue_frac_isolated"] = round(valu_cyc / (1024 * cyc), 4)
+            roof["profile_clock_ghz"] = round(ghz, 3)
         line = {
             "metric": "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s",
             "value": round(mrays, 2),
@@ -213,11 +242,7 @@ def main():
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_median": round(kern_median, 4),
             "kernel_mrays_per_s": round(W * H / world / (kern_ms * 1e-3) / 1e6, 2),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "achieved_isolated": round(achieved_isolated, 1),
-                         "frac_isolated": round(achieved_isolated / HBM_PEAK_GBS, 4),
-                         "algorithmic_bytes_per_launch": launch_bytes, "algorithmic_bytes_per_frame": frame_bytes},
+            "roofline": roof,
         }
         if frame_latency_ms is not None:
             line["frame_latency_ms"] = round(frame_latency_ms, 4)

@@ -40,6 +40,13 @@ def main():
     out = {"config": cfg, "world": 1, "kernel": kern, "fetch_kib_raw": f_kb, "write_kib_raw": w_kb,
            "hbm_bytes_per_launch": int((2 * f_kb + w_kb) * 1024),
            "rocprof_avg_ns": stats.get(kern, {}).get("avg_ns")}
+    # what does bound the kernel: VALU wave-instructions (2 cycles each on a SIMD-32)
+    # and the shader clock cycles (GRBM_GUI_ACTIVE sums the 8 XCDs) per launch
+    valu = per_dispatch(os.path.join(root, "pmc_sq"), "SQ_INSTS_VALU").get(kern)
+    grbm = per_dispatch(os.path.join(root, "pmc_tcc"), "GRBM_GUI_ACTIVE").get(kern)
+    if valu and grbm:
+        out["valu_insts_per_launch"] = statistics.median(valu)
+        out["grbm_gui_active_per_launch"] = statistics.median(grbm)
     print(json.dumps(out, indent=1))
 
 

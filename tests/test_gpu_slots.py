@@ -1,0 +1,56 @@
+"""GPU test of the per-launch scratch slots (vr_host.cpp SlotRing): the
+crawl-deferral list of a VCS tile launch and the work queue of a persistent
+launch.  Many launches in flight on several streams at once, far more of them
+than the ring has slots, must each render exactly the frame one serial launch
+renders: a slot shared by two launches in flight would mix their deferred
+records (wrong or zero pixels) or their queue heads."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+vr = pytest.importorskip("voxelraymarcher_amd")
+
+
+@pytest.fixture(scope="module")
+def c5_scene():
+    cfg = vr.CONFIGS["C5"]
+    xyz, rgb = cfg.voxels()
+    return cfg, vr.create_scene(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE)
+
+
+@pytest.mark.parametrize("kernel", [vr.Kernel.TILE, vr.Kernel.PERSISTENT], ids=lambda k: k.name)
+@pytest.mark.parametrize("algo", [vr.RayMarchAlgorithm.ORIGINAL, vr.RayMarchAlgorithm.LONGEST_AXIS],
+                         ids=lambda a: a.name)
+def test_launches_in_flight_on_three_streams(c5_scene, kernel, algo):
+    # C5 rows 696-712 defer thousands of crawling rays per launch (test_gpu_parity.test_c5_crawl_rows)
+    cfg, scene = c5_scene
+    W, H, r0, r1 = cfg.width, cfg.height, 696, 712
+    cam = vr.Camera.reference(W, H)
+    lit = vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    words = (r1 - r0) * W
+    ref = torch.full((words,), -1, dtype=torch.int32, device="cuda")
+    vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, ref, r0, r1, kernel=kernel)
+    torch.cuda.synchronize()
+    ref_np = ref.cpu().numpy()
+    assert np.count_nonzero(ref_np) > 0
+    depth, frames = 3, 70                       # 70 launches > the ring's 16 slots; 16 % 3 != 0
+    streams = [torch.cuda.Stream() for _ in range(depth)]
+    outs = [torch.full((words,), -1, dtype=torch.int32, device="cuda") for _ in range(frames)]
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream())
+    for i in range(frames):
+        vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, outs[i], r0, r1, stream=streams[i % depth],
+                                  kernel=kernel)
+    torch.cuda.synchronize()
+    bad = [i for i in range(frames) if not torch.equal(outs[i], ref)]
+    assert not bad, f"{len(bad)} of {frames} launches differ from the serial render (first: {bad[:5]})"
+    # the slots are clean afterwards: one more serial launch still matches
+    last = torch.full((words,), -1, dtype=torch.int32, device="cuda")
+    vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, last, r0, r1, kernel=kernel)
+    torch.cuda.synchronize()
+    assert torch.equal(last, ref)

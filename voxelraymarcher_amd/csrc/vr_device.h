@@ -62,16 +62,21 @@ __device__ __forceinline__ uint32_t f2u(float f) {
     return r;
 }
 
-// Correctly rounded n / d with the reciprocal half hoisted out of a walk.
-// hipcc's IEEE f32 division on gfx9 is
-//   ds = v_div_scale(d); r0 = v_rcp_f32(ds); r = fma(fma(-ds, r0, 1), r0, r0);
-//   ns = v_div_scale(n); q = ns * r; q = fma(fma(-ds, q, ns), r, q);
-//   q = v_div_fmas(fma(-ds, q, ns), r, q); v_div_fixup(q, d, n)
-// and for 2^-64 <= |d| <= 2^20 and 2^-90 <= |n| <= 2^20 the two div_scales are
-// the identity (VCC clear, so div_fmas is a plain fma) and div_fixup returns q:
-// div_fast() is that sequence with r computed once per direction, bit-identical
-// to n / d on that domain.  Callers test div_fast_ok() (or the bounds it
-// checks: inside a region walk |n| < 73 always) and fall back to `/`.
+// Correctly rounded n / d with the reciprocal hoisted out of a walk:
+//   r = fma(fma(-d, r0, 1), r0, r0), r0 = v_rcp_f32(d)     (once per direction)
+//   q = RN(n * r);  q' = fma(fma(-d, q, n), r, q) = RN(n / d)
+// (one Markstein correction: mul + 2 fma per division).  For normal n, d whose
+// intermediates stay normal every step scales exactly with the exponents, so
+// the result depends only on the two significands -- r included:
+// tools/div_proof.hip checks, on the device, that r(+-m 2^e) = +-r(m) 2^-e for
+// every significand m and every e of the domain, and all 2^23 x 2^23
+// significand pairs (n, d) against hipcc's IEEE division: 0 mismatches
+// (profiles/r02/div_proof.json; the same holds with r = RN(1/d)).  The domain
+// that keeps r, q and q' normal and the residual exact: 2^-64 <= |d| <= 2^20,
+// 2^-90 <= |n| <= 2^20; tools/div_check.hip re-checks every numerator of it for
+// a list of divisors.  Callers test div_fast_ok() (or the bounds it checks:
+// inside a region walk |n| < 73 always) and fall back to `/`.
+// (Round 1 ran hipcc's own sequence with the reciprocal half hoisted: mul + 4 fma.)
 struct Rcp { float d, r; bool ok; };
 __device__ __forceinline__ Rcp rcp_setup(float d) {
     const float r0 = __builtin_amdgcn_rcpf(d);
@@ -84,8 +89,7 @@ __device__ __forceinline__ bool div_fast_ok(float n, const Rcp& c) {
     return c.ok && a >= 0x1p-90f && a <= 0x1p+20f;
 }
 __device__ __forceinline__ float div_fast(float n, const Rcp& c) {
-    float q = n * c.r;
-    q = __builtin_fmaf(__builtin_fmaf(-c.d, q, n), c.r, q);
+    const float q = n * c.r;
     return __builtin_fmaf(__builtin_fmaf(-c.d, q, n), c.r, q);
 }
 // px ? ceilf(o) + EPSILON : floorf(o) - EPSILON, branch-free: with s = +-1,

@@ -434,91 +434,110 @@ int make_view(const vr_scene* s, const vr_camera* cam, const vr_lighting* lit, c
     return VR_OK;
 }
 
-// Per-device ring of persistent-kernel queue slots (vr::kQueueWords uint32
-// each, zeroed on the launch stream before every launch).  Launches in flight
-// at the same time (other streams) get different slots as long as fewer than
-// kQueueSlots are outstanding.
-constexpr uint32_t kQueueSlots = 256;
-struct QueueRing {
+// Per-device rings of device scratch slots that a launch borrows: the
+// crawl-deferral list of a tile launch (vr::kDeferWords uint32, zeroed once;
+// the crawl pass resets it at its end) and the work queue of a persistent
+// launch (vr::kQueueWords uint32, zeroed on the launch stream first).  A slot
+// belongs to ONE launch at a time: the launch that takes it waits (on its own
+// stream, hipStreamWaitEvent) for the event the slot's previous launch recorded
+// after its last kernel, and records the slot's event again after its own.  The
+// ring's lock is held from taking the slot to recording the event, so two
+// launches in flight -- on any streams, from any threads -- never share a slot
+// however many slots there are (a wait on an event of the same stream or one
+// that has completed costs nothing).
+struct SlotRing {
+    const char* name;
+    size_t words;          // uint32 per slot
+    uint32_t nslots;
     std::mutex mu;
-    uint32_t* base[64] = {nullptr};
-    std::atomic<uint32_t> next{0};
+    struct Dev {
+        uint32_t* base = nullptr;
+        std::vector<hipEvent_t> ev;
+        std::vector<bool> used;
+        uint32_t next = 0;
+    } dev[64];
+    SlotRing(const char* n, size_t w, uint32_t s) : name(n), words(w), nslots(s) {}
 };
-QueueRing g_ring;
+SlotRing g_defer_ring("defer ring", vr::kDeferWords, 16);
+SlotRing g_queue_ring("queue ring", vr::kQueueWords, 16);
 
-int queue_slot(int dev, uint32_t** out) {
-    if (dev < 0 || dev >= 64) return fail(VR_E_INVALID, "device index too large");
-    if (!g_ring.base[dev]) {
-        std::lock_guard<std::mutex> lk(g_ring.mu);
-        if (!g_ring.base[dev]) {
-            void* p = nullptr;
-            hipError_t e = hipMalloc(&p, (size_t)kQueueSlots * vr::kQueueWords * sizeof(uint32_t));
-            if (e != hipSuccess) return hip_fail(e, "hipMalloc(queue ring)");
-            e = hipMemset(p, 0, (size_t)kQueueSlots * vr::kQueueWords * sizeof(uint32_t));
-            if (e != hipSuccess) return hip_fail(e, "hipMemset(queue ring)");
-            e = hipDeviceSynchronize();
-            if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
-            g_ring.base[dev] = (uint32_t*)p;
+// The borrowed slot; the lock is held until release() (or destruction).
+struct SlotLease {
+    SlotRing* ring = nullptr;
+    std::unique_lock<std::mutex> lk;
+    int dev = -1;
+    uint32_t idx = 0;
+    uint32_t* p = nullptr;
+    int acquire(SlotRing& r, int d, hipStream_t stream) {
+        if (d < 0 || d >= 64) return fail(VR_E_INVALID, "device index too large");
+        ring = &r;
+        lk = std::unique_lock<std::mutex>(r.mu);
+        SlotRing::Dev& D = r.dev[d];
+        if (!D.base) {
+            void* q = nullptr;
+            const size_t bytes = (size_t)r.nslots * r.words * sizeof(uint32_t);
+            hipError_t e = hipMalloc(&q, bytes);
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(slot ring)");
+            e = hipMemset(q, 0, bytes);
+            if (e == hipSuccess) e = hipDeviceSynchronize();
+            if (e != hipSuccess) { (void)hipFree(q); return hip_fail(e, "hipMemset(slot ring)"); }
+            D.ev.assign(r.nslots, nullptr);
+            for (uint32_t i = 0; i < r.nslots; ++i) {
+                e = hipEventCreateWithFlags(&D.ev[i], hipEventDisableTiming);
+                if (e != hipSuccess) return hip_fail(e, "hipEventCreate(slot ring)");
+            }
+            D.used.assign(r.nslots, false);
+            D.base = (uint32_t*)q;
         }
+        dev = d;
+        idx = D.next;
+        D.next = (D.next + 1u) % r.nslots;
+        if (D.used[idx]) {
+            hipError_t e = hipStreamWaitEvent(stream, D.ev[idx], 0);
+            if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent(slot ring)");
+        }
+        p = D.base + r.words * idx;
+        return VR_OK;
     }
-    *out = g_ring.base[dev] + (size_t)vr::kQueueWords * (g_ring.next.fetch_add(1) % kQueueSlots);
-    return VR_OK;
-}
-
-// Per-device ring of crawl-deferral slots (vr::kDeferWords uint32 each, zeroed
-// once; the crawl pass resets its slot at its end), one per launch in flight.
-constexpr uint32_t kDeferSlots = 64;
-struct DeferRing {
-    std::mutex mu;
-    uint32_t* base[64] = {nullptr};
-    std::atomic<uint32_t> next{0};
+    // after the launch's last kernel on `stream`
+    int release(hipStream_t stream) {
+        SlotRing::Dev& D = ring->dev[dev];
+        hipError_t e = hipEventRecord(D.ev[idx], stream);
+        if (e != hipSuccess) return hip_fail(e, "hipEventRecord(slot ring)");
+        D.used[idx] = true;
+        lk.unlock();
+        return VR_OK;
+    }
 };
-DeferRing g_defer;
-
-int defer_slot(int dev, uint32_t** out) {
-    if (dev < 0 || dev >= 64) return fail(VR_E_INVALID, "device index too large");
-    if (!g_defer.base[dev]) {
-        std::lock_guard<std::mutex> lk(g_defer.mu);
-        if (!g_defer.base[dev]) {
-            void* p = nullptr;
-            const size_t bytes = (size_t)kDeferSlots * vr::kDeferWords * sizeof(uint32_t);
-            hipError_t e = hipMalloc(&p, bytes);
-            if (e != hipSuccess) return hip_fail(e, "hipMalloc(defer ring)");
-            e = hipMemset(p, 0, bytes);
-            if (e != hipSuccess) return hip_fail(e, "hipMemset(defer ring)");
-            e = hipDeviceSynchronize();
-            if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
-            g_defer.base[dev] = (uint32_t*)p;
-        }
-    }
-    *out = g_defer.base[dev] + (size_t)vr::kDeferWords * (g_defer.next.fetch_add(1) % kDeferSlots);
-    return VR_OK;
-}
 
 int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void* stream) {
     if (algo != VR_ALGO_ORIGINAL && algo != VR_ALGO_LONGESTAXIS) return fail(VR_E_INVALID, "unknown algorithm");
     if (v.local_rows == 0 || v.W == 0) return VR_OK;
     DeviceGuard dg(s->device);
     const bool count = v.bytes != nullptr;
+    const hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     if (kernel == VR_KERNEL_AUTO) kernel = VR_KERNEL_TILE;   // measured fastest for every pair
     v.crawl_rewalk = kernel == VR_KERNEL_TILE_REWALK ? 1u : 0u;
     if (kernel == VR_KERNEL_TILE_REWALK) kernel = VR_KERNEL_TILE;
+    SlotLease lease;
     if (kernel == VR_KERNEL_TILE) {
         if (s->store == VR_STORE_VCS) {           // cluster-skip crawls: deferred to a second pass
-            int rc = defer_slot(s->device, &v.defer);
+            int rc = lease.acquire(g_defer_ring, s->device, st);
             if (rc) return rc;
+            v.defer = lease.p;
             v.defer_cap = vr::kDeferCap;
         }
-        e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, (hipStream_t)stream);
+        e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st);
     } else {
-        uint32_t* q = nullptr;
-        int rc = queue_slot(s->device, &q);
+        int rc = lease.acquire(g_queue_ring, s->device, st);
         if (rc) return rc;
-        e = vr::launch_persist((int)s->store, (int)algo, count, kscene(s), v, q, (hipStream_t)stream);
+        e = vr::launch_persist((int)s->store, (int)algo, count, kscene(s), v, lease.p, st);
     }
+    // (on a failed launch the slot is still fenced: a kernel of it may be queued)
+    const int rc = lease.ring ? lease.release(st) : VR_OK;
     if (e != hipSuccess) return hip_fail(e, "ray-march launch");
-    return VR_OK;
+    return rc;
 }
 
 // ------------------------------------------------------------- synthetic grid

@@ -66,7 +66,13 @@ struct KView {
 // tile pass are deferred to a second pass over a per-launch list.
 // A slot is [count, done, 0, 0] and kDeferCap records of kDeferRecWords words:
 // the crawling walk's state at the crawl (vr_march.hip, grid_original_rt), from
-// which the crawl pass resumes it.
+// which the crawl pass resumes it.  Record words:
+//   0 pixel (row << 16 | x)   1 flags (1 shadow walk, 2 longest-axis shadow, 4 walk from the start)
+//   2-4 stepped position      5-7 region         8 unused (0)
+//   9 iterations so far       10 counted bytes so far
+//   11-13 tX, tY, tZ of the last voxel step (hit normal; 0 for shadow walks)
+//   14 reserved (0)           15-17 the crawl iteration's voxel   18 lit colour   19 unused
+// A slot is used by one launch at a time (vr_host.cpp SlotRing).
 constexpr uint32_t kDeferCap = 16384;
 constexpr uint32_t kDeferRecWords = 20;
 constexpr uint32_t kDeferWords = 4 + kDeferCap * kDeferRecWords;

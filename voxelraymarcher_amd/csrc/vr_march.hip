@@ -177,16 +177,14 @@ struct Walker : Ctx<STORE, COUNT> {
         float nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
         float nY = py ? ceilf(o.y) + kEps : floorf(o.y) - kEps;
         float nZ = pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps;
-        float tX, tY, tZ, tMin;
+        float tX, tY, tZ;
         if (resume) {                             // o is the stepped position of the crawl
-            tX = __uint_as_float(rs[11]); tY = __uint_as_float(rs[12]);
-            tZ = __uint_as_float(rs[13]); tMin = __uint_as_float(rs[14]);
+            tX = __uint_as_float(rs[11]); tY = __uint_as_float(rs[12]); tZ = __uint_as_float(rs[13]);
         } else {
             tX = zx ? kInf : (nX - o.x) / d.x;
             tY = zy ? kInf : (nY - o.y) / d.y;
             tZ = zz ? kInf : (nZ - o.z) / d.z;
-            tMin = fminf(tX, fminf(tY, tZ));
-            o = add(o, scl(tMin + kEps, d));
+            o = add(o, scl(fminf(tX, fminf(tY, tZ)) + kEps, d));
         }
         uint32_t col = kEmpty;
         if constexpr (STORE == STORE_VCS) {
@@ -248,6 +246,7 @@ struct Walker : Ctx<STORE, COUNT> {
                             this->count(4);
                             const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
                             blk = mreg[wi];
+                            __builtin_amdgcn_sched_barrier(0);   // issue the load before the planes
                             // both candidate planes, computed while the mask word is in
                             // flight and materialised (with the whole 8-B word: one load)
                             float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey), vZ = plane_v<SZ>(o.z, gz, ez);
@@ -367,7 +366,7 @@ struct Walker : Ctx<STORE, COUNT> {
                             r[10] = this->bytes;
                             // (a shadow walk has no normal: its t values are not kept live for this)
                             r[11] = SHADOW ? 0u : __float_as_uint(tX); r[12] = SHADOW ? 0u : __float_as_uint(tY);
-                            r[13] = SHADOW ? 0u : __float_as_uint(tZ); r[14] = SHADOW ? 0u : __float_as_uint(fminf(tX, fminf(tY, tZ)));
+                            r[13] = SHADOW ? 0u : __float_as_uint(tZ); r[14] = 0u;   // reserved
                             // The crawl iteration's voxel q (see crawl_voxel): recovered from
                             // the stepped position; if it cannot be, the crawl pass walks the
                             // pixel from its start instead.
