@@ -17,6 +17,20 @@
 // only on (hit origin, region, shadow algorithm), so the pixel is identical.
 #include "vr_device.h"
 
+// VR_DIAG (profiling builds only, profiles/wave_counts.py): wave-level execution
+// counters -- one atomic per wave per counted event, from the wave's first
+// active lane.  Never part of the library build.
+#ifdef VR_DIAG
+__device__ unsigned long long g_vr_diag[32];
+#define VR_DIAG_COUNT(k)                                                              \
+    do {                                                                             \
+        if (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) \
+            atomicAdd(&g_vr_diag[(k)], 1ull);                                        \
+    } while (0)
+#else
+#define VR_DIAG_COUNT(k) do { } while (0)
+#endif
+
 namespace vr {
 namespace {
 
@@ -172,6 +186,7 @@ struct Walker : Ctx<STORE, COUNT> {
     __device__ __forceinline__ bool grid_original_rt(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h, const bool SHADOW,
                                                      const bool EQ, const uint32_t* rs = nullptr) {
         const bool resume = CRAWL && rs != nullptr;
+        VR_DIAG_COUNT(SHADOW ? 9 : 8);                 // grid_original calls
         const bool px = d.x > 0.0f, py = d.y > 0.0f, pz = d.z > 0.0f;
         const bool zx = SHADOW && d.x == 0.0f, zy = SHADOW && d.y == 0.0f, zz = SHADOW && d.z == 0.0f;
         float nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
@@ -240,8 +255,14 @@ struct Walker : Ctx<STORE, COUNT> {
                     // then need no sign multiplications (see plane_v / plane_c8).
                     auto walk = [&](auto SXc, auto SYc, auto SZc) {
                         constexpr int SX = decltype(SXc)::value, SY = decltype(SYc)::value, SZ = decltype(SZc)::value;
+                        // The iteration count as the budget test reads it, biased so that
+                        // it reaches bits(64.0f) exactly when iters exceeds kIterBudget:
+                        // one add per iteration.
+                        uint32_t ic = this->iters + (0x42800000u - kIterBudget);
+                        VR_DIAG_COUNT((SHADOW ? 4 : 0) + (SX == 0 ? 1 : 0));   // walk entries
                         for (;;) {
-                            ++this->iters;
+                            ++ic;
+                            VR_DIAG_COUNT((SHADOW ? 6 : 2) + (SX == 0 ? 1 : 0));   // loop iterations
                             const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
                             this->count(4);
                             const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
@@ -276,7 +297,7 @@ struct Walker : Ctx<STORE, COUNT> {
                                 if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
                                     sMin = bad ? am / fabsf(d.x) : sMin;
                                     crawl = bad & walk_ok & skip & (sMin == 0.0f) &
-                                            (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                                            (CRAWL ? ic - (0x42800000u - kIterBudget) >= crawl_after : !crawl_off);
                                     if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
                                 }
                             } else {
@@ -289,25 +310,24 @@ struct Walker : Ctx<STORE, COUNT> {
                                     // a skip step with t = 0 (its plane axis has n = 0, so it is
                                     // always on this branch): the ray creeps through an empty cluster
                                     crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
-                                            (CRAWL ? this->iters >= crawl_after : !crawl_off);
+                                            (CRAWL ? ic - (0x42800000u - kIterBudget) >= crawl_after : !crawl_off);
                                     if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
                                 }
                                 sMin = fminf(sX, fminf(sY, sZ));
                                 const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
                                 tX = vox ? sX : tX; tY = vox ? sY : tY; tZ = vox ? sZ : tZ;   // (tMin: min of the three, at the use)
                             }
-                            const f3 on = EQ ? add(o, f3{(sMin + kEps) * d.x, (sMin + kEps) * d.x, (sMin + kEps) * d.x})
-                                             : add(o, scl(sMin + kEps, d));
-                            // a hit keeps o unstepped (bit-select on the hit mask)
-                            o.x = bit_select(fm, o.x, on.x);
-                            o.y = bit_select(fm, o.y, on.y);
-                            o.z = bit_select(fm, o.z, on.z);
+                            // A hit keeps o unstepped: its step length becomes (-EPSILON) + EPSILON
+                            // = +0 exactly, and o + (+0 * d) = o (o is never -0, d is finite in here).
+                            const float ts = bit_select(fm, -kEps, sMin) + kEps;
+                            o = EQ ? add(o, f3{ts * d.x, ts * d.x, ts * d.x}) : add(o, scl(ts, d));
                             // One unsigned compare for hit, region exit (in_region_bits_nz of the
                             // stepped position) and the budget (iters >= kIterBudget):
-                            const uint32_t ev = max(max(max(max(__float_as_uint(on.x), __float_as_uint(on.y)), __float_as_uint(on.z)),
-                                                        this->iters + (0x42800000u - kIterBudget)), fm);
+                            const uint32_t ev = max(max(max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)),
+                                                        ic), fm);
                             if (ev >= 0x42800000u || crawl) break;
                         }
+                        this->iters = ic - (0x42800000u - kIterBudget);
                     };
                     const uint32_t sg = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
                     const uint32_t sg0 = __builtin_amdgcn_readfirstlane(sg);
@@ -433,8 +453,9 @@ struct Walker : Ctx<STORE, COUNT> {
             const float nlim = walk_ok ? 0x1p-90f : kInf;
             uint32_t key = 0;
             uint2 e1{0u, 0u}, e2{0u, 0u};
+            uint32_t ic = this->iters + (0x42800000u - kIterBudget);   // biased count (see the VCS walk)
             for (;;) {
-                ++this->iters;
+                ++ic;
                 const uint32_t vx = (uint32_t)f2i(o.x), vy = (uint32_t)f2i(o.y), vz = (uint32_t)f2i(o.z);
                 key = lshl_or(lshl_or(vx, 10u, vy), 10u, vz);              // generate3DPoint (x<<20|y<<10|z)
                 e1 = t1[fastmod(hash1(key, m.w), fmod)];
@@ -458,8 +479,6 @@ struct Walker : Ctx<STORE, COUNT> {
                     }
                     sMin = fminf(sX, fminf(sY, sZ));
                 }
-                const f3 on = EQ ? add(o, f3{(sMin + kEps) * d.x, (sMin + kEps) * d.x, (sMin + kEps) * d.x})
-                                 : add(o, scl(sMin + kEps, d));
                 // CuckooHashTable::lookupVoxel (CuckooHashTable.cuh:59-76): key1 (+val1 on a
                 // match), else key2 (+val2 on a match)
                 const bool m1 = e1.x == key, m2 = e2.x == key;
@@ -468,13 +487,13 @@ struct Walker : Ctx<STORE, COUNT> {
                 if (!SHADOW && !EQ) {                     // a non-hit step: its t values feed the normal
                     tX = fm ? tX : sX; tY = fm ? tY : sY; tZ = fm ? tZ : sZ;
                 }
-                o.x = bit_select(fm, o.x, on.x);
-                o.y = bit_select(fm, o.y, on.y);
-                o.z = bit_select(fm, o.z, on.z);
-                const uint32_t ev = max(max(max(max(__float_as_uint(on.x), __float_as_uint(on.y)), __float_as_uint(on.z)),
-                                            this->iters + (0x42800000u - kIterBudget)), fm);
+                // a hit keeps o unstepped: step length (-EPSILON) + EPSILON = +0 (see the VCS walk)
+                const float ts = bit_select(fm, -kEps, sMin) + kEps;
+                o = EQ ? add(o, f3{ts * d.x, ts * d.x, ts * d.x}) : add(o, scl(ts, d));
+                const uint32_t ev = max(max(max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)), ic), fm);
                 if (ev >= 0x42800000u) break;
             }
+            this->iters = ic - (0x42800000u - kIterBudget);
             // why the lane left (see the VCS walk): recomputed from VGPR values
             asm("" : "+v"(e1.x), "+v"(e1.y), "+v"(e2.x), "+v"(e2.y), "+v"(key), "+v"(o.x), "+v"(o.y), "+v"(o.z));
             const bool m1 = e1.x == key, found = m1 || e2.x == key;
@@ -827,8 +846,10 @@ struct Walker : Ctx<STORE, COUNT> {
         f3 so = scl(v.scale_f, sub(wo, tr));      // Ray::convertRayToLocalSpace (Ray.cuh:14-17)
         f3 d = wd;
         i3 cr{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
+        VR_DIAG_COUNT(14);                            // primary() calls
         while (!in_scene(cr)) {                   // entry clip (:349-373)
             if (!tick()) return false;
+            VR_DIAG_COUNT(15);
             int32_t hi = (int32_t)(s.D + (uint32_t)s.min_coord), lo = s.min_coord;
             int32_t nx = d.x < 0.0f ? hi : lo, ny = d.y < 0.0f ? hi : lo, nz = d.z < 0.0f ? hi : lo;
             float tX = ((float)(nx * kBlock) - so.x) / d.x;
@@ -857,9 +878,11 @@ struct Walker : Ctx<STORE, COUNT> {
         }
         while (in_scene(cr)) {
             if (!tick()) return false;
+            VR_DIAG_COUNT(10);                         // primary region rounds
             uint32_t reg = region_at(cr);
             while (reg == kNone) {
                 if (!tick()) return false;
+                VR_DIAG_COUNT(11);                     // null-region skips
                 if (!this->template skip_null<false>(cr, o, d, reg)) return false;
             }
             bool hit = ALGO == ALGO_ORIGINAL ? grid_original<false>(o, d, reg, cr, h)
@@ -886,9 +909,11 @@ struct Walker : Ctx<STORE, COUNT> {
         }
         while (in_scene(cr)) {
             if (!tick()) return false;
+            VR_DIAG_COUNT(12);                         // shadow region rounds
             uint32_t reg = region_at(cr);
             while (reg == kNone) {
                 if (!tick()) return false;
+                VR_DIAG_COUNT(13);
                 if (!this->template skip_null<!LONGEST>(cr, o, d, reg)) return false;
             }
             bool hit = LONGEST ? (STORE == STORE_VCS ? grid_longest_vcs<true>(o, d, reg, cr, dummy)
@@ -924,6 +949,7 @@ __device__ __forceinline__ uint32_t light_and_shadow(Walker<STORE, COUNT, CRAWL>
                                               (float)(h.region.z * kBlock)));
     const uint32_t lit = w.lighting(h.col, h.n, rwp, h.so);
     if (v.use_shadows) {
+        VR_DIAG_COUNT(16);                             // shadow walks started
         w.lit_saved = lit;
         const bool eq = v.L[0] == v.L[1] && v.L[1] == v.L[2];
         if (h.longest) {
@@ -1085,3 +1111,15 @@ hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hip
 }
 
 }  // namespace vr
+
+#ifdef VR_DIAG
+extern "C" int vr_diag_fetch(unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vr_diag), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_vr_diag), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
