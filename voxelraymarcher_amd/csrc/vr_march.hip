@@ -157,6 +157,11 @@ struct Walker : Ctx<STORE, COUNT> {
     using C::lighting; using C::normal_from_t; using C::in_region; using C::grid_in_region;
     using C::advance_region; using C::in_scene; using C::region_at; using C::skip_null; using C::bytes;
     __device__ Walker(const KScene& s_, const KView& v_) : C(s_, v_) {}
+    // Per-ray reciprocals for the entry clip and each region walk's initial step
+    // (div_fast instead of IEEE division): cuckoo C4 -2.5 %, but the VCS walks'
+    // kernel runs at its 72-VGPR limit and the longer-lived values cost spills
+    // there (C2 +1.6 %, C3 +4 %), so VCS keeps the plain divisions.
+    static constexpr bool kFastSetup = STORE == STORE_HASH;
     // what a deferred crawl must know to be resumed (see the deferral below):
     // bit 1 = the shadow walk is the longest-axis one; the lit colour of the hit
     uint32_t ctx = 0, lit_saved = 0;
@@ -177,25 +182,46 @@ struct Walker : Ctx<STORE, COUNT> {
     // one product.  Bit-identical; shadow walks read no per-axis t values.
     template <bool SHADOW, bool EQ = false>
     __device__ __forceinline__ bool grid_original(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h,
-                                                  const uint32_t* rs = nullptr) {
-        return grid_original_rt(o, d, reg, cr, h, SHADOW, SHADOW && EQ, rs);
+                                                  const uint32_t* rs = nullptr, const Rcp* rc = nullptr) {
+        return grid_original_rt(o, d, reg, cr, h, SHADOW, SHADOW && EQ, rs, rc);
     }
     // The same with the shadow flag a per-lane value (fused primary + shadow
     // walk); the template form above constant-folds it.
     // rs (crawl pass only): a deferral record -- resume the walk at its crawl.
+    // rc: the ray's reciprocals rcp_setup(d.x), (d.y), (d.z), made once per ray
+    // (nullptr: made here).
     __device__ __forceinline__ bool grid_original_rt(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h, const bool SHADOW,
-                                                     const bool EQ, const uint32_t* rs = nullptr) {
+                                                     const bool EQ, const uint32_t* rs = nullptr,
+                                                     const Rcp* rc = nullptr) {
         const bool resume = CRAWL && rs != nullptr;
         VR_DIAG_COUNT(SHADOW ? 9 : 8);                 // grid_original calls
         const bool px = d.x > 0.0f, py = d.y > 0.0f, pz = d.z > 0.0f;
         const bool zx = SHADOW && d.x == 0.0f, zy = SHADOW && d.y == 0.0f, zz = SHADOW && d.z == 0.0f;
-        float nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
-        float nY = py ? ceilf(o.y) + kEps : floorf(o.y) - kEps;
-        float nZ = pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps;
         float tX, tY, tZ;
         if (resume) {                             // o is the stepped position of the crawl
             tX = __uint_as_float(rs[11]); tY = __uint_as_float(rs[12]); tZ = __uint_as_float(rs[13]);
+        } else if (!CRAWL && kFastSetup) {
+            // The initial step (Renderer.cuh:269-280; shadow :106-117) with the ray's
+            // hoisted reciprocals: |n| <= 1 + EPSILON here, so the fast division's
+            // domain is the direction's plus |n| >= 2^-90 (see div_fast).
+            const Rcp r0x = rc ? rc[0] : rcp_setup(d.x), r0y = rc ? rc[1] : rcp_setup(d.y),
+                      r0z = rc ? rc[2] : rcp_setup(d.z);
+            const float sx = px ? 1.0f : -1.0f, sy = py ? 1.0f : -1.0f, sz = pz ? 1.0f : -1.0f;
+            const float ax = next_plane_fma(o.x, sx, sx * kEps) - o.x, ay = next_plane_fma(o.y, sy, sy * kEps) - o.y,
+                        az = next_plane_fma(o.z, sz, sz * kEps) - o.z;
+            const bool fast = r0x.ok && r0y.ok && r0z.ok && !zx && !zy && !zz &&
+                              fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= 0x1p-90f;
+            tX = div_fast(ax, r0x); tY = div_fast(ay, r0y); tZ = div_fast(az, r0z);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(!fast) != 0, 0)) {
+                tX = fast ? tX : (zx ? kInf : ax / d.x);
+                tY = fast ? tY : (zy ? kInf : ay / d.y);
+                tZ = fast ? tZ : (zz ? kInf : az / d.z);
+            }
+            o = add(o, scl(fminf(tX, fminf(tY, tZ)) + kEps, d));
         } else {
+            const float nX = px ? ceilf(o.x) + kEps : floorf(o.x) - kEps;
+            const float nY = py ? ceilf(o.y) + kEps : floorf(o.y) - kEps;
+            const float nZ = pz ? ceilf(o.z) + kEps : floorf(o.z) - kEps;
             tX = zx ? kInf : (nX - o.x) / d.x;
             tY = zy ? kInf : (nY - o.y) / d.y;
             tZ = zz ? kInf : (nZ - o.z) / d.z;
@@ -231,8 +257,16 @@ struct Walker : Ctx<STORE, COUNT> {
                 // being hoisted).
                 f3 dl = d;
                 if (CRAWL) asm("" : "+v"(dl.x), "+v"(dl.y), "+v"(dl.z));
-                // Hoisted reciprocals (div_fast) and +-1 plane signs for the loop.
-                const Rcp rx = rcp_setup(EQ ? fabsf(dl.x) : dl.x), ry = rcp_setup(dl.y), rz = rcp_setup(dl.z);
+                // Hoisted reciprocals (div_fast) and +-1 plane signs for the loop
+                // (rcp_setup(-d) = -rcp_setup(d) bit for bit: tools/div_proof.hip).
+                Rcp rx, ry, rz;
+                if (rc && !CRAWL && kFastSetup) {
+                    rx = EQ ? Rcp{fabsf(dl.x), fabsf(rc[0].r), rc[0].ok} : rc[0];
+                    ry = rc[1];
+                    rz = rc[2];
+                } else {
+                    rx = rcp_setup(EQ ? fabsf(dl.x) : dl.x); ry = rcp_setup(dl.y); rz = rcp_setup(dl.z);
+                }
                 const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
                 const float ex = gx * kEps, ey = gy * kEps, ez = gz * kEps;
                 const int32_t cx8 = px ? 8 : 0, cy8 = py ? 8 : 0, cz8 = pz ? 8 : 0;
@@ -282,9 +316,9 @@ struct Walker : Ctx<STORE, COUNT> {
                             found = fm != 0u;
                             vi = blk.y + __popc(blk.x & ((1u << (bit & 31u)) - 1u));
                             if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
-                            nX = skip ? cX : vX;
-                            nY = skip ? cY : vY;
-                            nZ = skip ? cZ : vZ;
+                            const float nX = skip ? cX : vX;
+                            const float nY = skip ? cY : vY;
+                            const float nZ = skip ? cZ : vZ;
                             const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
                             float sMin;
                             crawl = false;
@@ -845,6 +879,9 @@ struct Walker : Ctx<STORE, COUNT> {
         f3 tr = ld3(v.translation);
         f3 so = scl(v.scale_f, sub(wo, tr));      // Ray::convertRayToLocalSpace (Ray.cuh:14-17)
         f3 d = wd;
+        // the ray's reciprocals, made once for every division by d (div_fast; cuckoo
+        // store only, see kFastSetup)
+        const Rcp rc[3] = {rcp_setup(d.x), rcp_setup(d.y), rcp_setup(d.z)};
         i3 cr{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
         VR_DIAG_COUNT(14);                            // primary() calls
         while (!in_scene(cr)) {                   // entry clip (:349-373)
@@ -852,9 +889,19 @@ struct Walker : Ctx<STORE, COUNT> {
             VR_DIAG_COUNT(15);
             int32_t hi = (int32_t)(s.D + (uint32_t)s.min_coord), lo = s.min_coord;
             int32_t nx = d.x < 0.0f ? hi : lo, ny = d.y < 0.0f ? hi : lo, nz = d.z < 0.0f ? hi : lo;
-            float tX = ((float)(nx * kBlock) - so.x) / d.x;
-            float tY = ((float)(ny * kBlock) - so.y) / d.y;
-            float tZ = ((float)(nz * kBlock) - so.z) / d.z;
+            const float ax = (float)(nx * kBlock) - so.x, ay = (float)(ny * kBlock) - so.y,
+                        az = (float)(nz * kBlock) - so.z;
+            float tX = div_fast(ax, rc[0]), tY = div_fast(ay, rc[1]), tZ = div_fast(az, rc[2]);
+            // (a numerator is never -0 here; +0 divides exactly)
+            const bool fast = kFastSetup &&
+                              (__float_as_uint(ax) == 0u || div_fast_ok(ax, rc[0])) &&
+                              (__float_as_uint(ay) == 0u || div_fast_ok(ay, rc[1])) &&
+                              (__float_as_uint(az) == 0u || div_fast_ok(az, rc[2]));
+            if (!kFastSetup || __builtin_expect(__builtin_amdgcn_ballot_w64(!fast) != 0, 0)) {
+                tX = fast ? tX : ax / d.x;
+                tY = fast ? tY : ay / d.y;
+                tZ = fast ? tZ : az / d.z;
+            }
             if (tX <= 0.0f) tX = kInf;
             if (tY <= 0.0f) tY = kInf;
             if (tZ <= 0.0f) tZ = kInf;
@@ -864,12 +911,13 @@ struct Walker : Ctx<STORE, COUNT> {
             cr = i3{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
         }
         f3 o = sub(so, mk((float)(cr.x * kBlock), (float)(cr.y * kBlock), (float)(cr.z * kBlock)));
-        return primary_regions<ALGO>(o, d, cr, h, nullptr);
+        return primary_regions<ALGO>(o, d, cr, h, nullptr, rc);
     }
     // The region walk of rayMarchVoxelScene(LongestAxis) (:376-433); rs (crawl
     // pass): first finish the region walk a deferral record left at its crawl.
     template <int ALGO>
-    __device__ __forceinline__ bool primary_regions(f3 o, f3 d, i3 cr, Hit& h, const uint32_t* rs) {
+    __device__ __forceinline__ bool primary_regions(f3 o, f3 d, i3 cr, Hit& h, const uint32_t* rs,
+                                                    const Rcp* rc = nullptr) {
         if (CRAWL && rs != nullptr) {
             const bool hit = grid_original_rt(o, d, this->region_at_nocount(cr), cr, h, false, false, rs);
             if (aborted) return false;
@@ -885,7 +933,7 @@ struct Walker : Ctx<STORE, COUNT> {
                 VR_DIAG_COUNT(11);                     // null-region skips
                 if (!this->template skip_null<false>(cr, o, d, reg)) return false;
             }
-            bool hit = ALGO == ALGO_ORIGINAL ? grid_original<false>(o, d, reg, cr, h)
+            bool hit = ALGO == ALGO_ORIGINAL ? grid_original<false>(o, d, reg, cr, h, nullptr, rc)
                                              : (STORE == STORE_VCS ? grid_longest_vcs<false>(o, d, reg, cr, h)
                                                                    : grid_longest<false>(o, d, reg, cr, h));
             if (aborted) return false;
@@ -900,6 +948,7 @@ struct Walker : Ctx<STORE, COUNT> {
     template <bool LONGEST, bool EQ = false>
     __device__ __forceinline__ bool shadow(f3 o, i3 cr, const uint32_t* rs = nullptr) {
         f3 d = ld3(v.L);
+        const Rcp rc[3] = {rcp_setup(d.x), rcp_setup(d.y), rcp_setup(d.z)};   // once per shadow ray
         Hit dummy;
         if (CRAWL && rs != nullptr) {            // resume a deferred crawl (as primary_regions)
             const bool hit = grid_original_rt(o, d, this->region_at_nocount(cr), cr, dummy, true, EQ, rs);
@@ -918,7 +967,7 @@ struct Walker : Ctx<STORE, COUNT> {
             }
             bool hit = LONGEST ? (STORE == STORE_VCS ? grid_longest_vcs<true>(o, d, reg, cr, dummy)
                                                      : grid_longest<true>(o, d, reg, cr, dummy))
-                               : grid_original<true, EQ>(o, d, reg, cr, dummy);
+                               : grid_original<true, EQ>(o, d, reg, cr, dummy, nullptr, rc);
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
@@ -929,14 +978,32 @@ struct Walker : Ctx<STORE, COUNT> {
 
 // calculateWorldRay (Renderer.cuh:1013-1022) + Camera::generateRay (Camera.cuh:25-29)
 // for pixel (x, local row l); false when the row is outside the frame.
+// FAST (cuckoo store, see Walker::kFastSetup): divisions with hoisted reciprocals.
+template <bool FAST>
 __device__ __forceinline__ bool pixel_ray(const KView& v, uint32_t x, uint32_t l, f3& ro, f3& rd) {
     const uint32_t band = l / v.band_rows;
     const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
     if (y >= v.row_limit) return false;
-    float u = ((float)x + 0.5f) / (float)v.W;
-    float vv = ((float)(v.H - y) + 0.5f) / (float)v.H;
+    if (!FAST) {
+        float u = ((float)x + 0.5f) / (float)v.W;
+        float vv = ((float)(v.H - y) + 0.5f) / (float)v.H;
+        ro = add(add(ld3(v.llc), scl(u, ld3(v.hor))), scl(vv, ld3(v.ver)));
+        rd = unit(sub(ro, ld3(v.org)));
+        return true;
+    }
+    // correctly rounded divisions by W, H (in [1, 65536]) and |ro - eye| with
+    // hoisted reciprocals (div_fast; its domain holds for u and v: numerators
+    // in [0.5, 65536])
+    const Rcp rW = rcp_setup((float)v.W), rH = rcp_setup((float)v.H);
+    float u = div_fast((float)x + 0.5f, rW);
+    float vv = div_fast((float)(v.H - y) + 0.5f, rH);
     ro = add(add(ld3(v.llc), scl(u, ld3(v.hor))), scl(vv, ld3(v.ver)));
-    rd = unit(sub(ro, ld3(v.org)));
+    const f3 c = sub(ro, ld3(v.org));                  // Vector3::normalize (Vector3.cuh:162, :79)
+    const float len = sqrtf(c.x * c.x + c.y * c.y + c.z * c.z);
+    const Rcp rl = rcp_setup(len);
+    auto okn = [&](float n) { return __float_as_uint(n) == 0u || div_fast_ok(n, rl); };
+    rd = f3{div_fast(c.x, rl), div_fast(c.y, rl), div_fast(c.z, rl)};
+    if (!(okn(c.x) && okn(c.y) && okn(c.z))) rd = f3{c.x / len, c.y / len, c.z / len};
     return true;
 }
 
@@ -971,7 +1038,7 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, const
     uint32_t col = 0;
     bytes = 0;
     f3 ro, rd;
-    if (pixel_ray(v, x, l, ro, rd)) {
+    if (pixel_ray<STORE == STORE_HASH>(v, x, l, ro, rd)) {
         Walker<STORE, COUNT, CRAWL> w(s, v);
         w.inv255 = inv255;
         Hit h;
@@ -997,7 +1064,7 @@ __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v
     uint32_t col = 0;
     if (!(r[1] & 1u)) {                           // the primary walk crawled
         f3 ro, rd;
-        pixel_ray(v, x, l, ro, rd);
+        pixel_ray<STORE == STORE_HASH>(v, x, l, ro, rd);
         Hit h;
         if (w.template primary_regions<ALGO>(o, rd, cr, h, r)) col = light_and_shadow(w, v, h);
     } else {                                      // the shadow walk crawled
