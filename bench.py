@@ -138,8 +138,13 @@ def main():
     pipe.drain()
     torch.cuda.synchronize()
 
-    # kernel-only timing of this rank's launch on the launch stream (HIP events)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # kernel-only timing of this rank's launch on the launch stream (HIP events),
+    # at least 200 launches (~35 ms of C2 work): enough samples for kernel_ms, and
+    # the GPU reaches its loaded clock before the timed loop starts (a short
+    # --steps run otherwise measures the clock ramp of a GPU that sat idle while
+    # the host built the scene)
+    n_iso = max(args.steps, 200)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_iso)]
     for a, b in ev:
         a.record(stream)
         render(pipe.bufs[0])

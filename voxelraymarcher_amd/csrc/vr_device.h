@@ -152,12 +152,13 @@ __device__ __forceinline__ uint32_t hash2(uint32_t k, uint32_t prime) {
     return k;
 }
 
-// Fill the workgroup's 256-entry table of (float)c / 255.0f (correctly rounded
-// division, same as VoxelFunctions.cuh:71-73) -- all threads must call it.
-__device__ __forceinline__ const float* load_inv255(float* lds) {
-    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) lds[i] = (float)i / 255.0f;
-    __syncthreads();
-    return lds;
+// (float)c / 255.0f, correctly rounded (VoxelFunctions.cuh:71-73), for c in
+// [0, 255]: div_fast with the correctly rounded reciprocal RN(1/255) (a
+// compile-time constant), exact on this domain (tools/div_proof.hip; c = 0
+// gives +0 as the division does).  Round 1 filled a 256-entry LDS table per
+// workgroup: ~140 VALU per wave and a barrier at every kernel start.
+__device__ __forceinline__ float div255(uint32_t c) {
+    return div_fast((float)c, Rcp{255.0f, 1.0f / 255.0f, true});
 }
 
 // VCS: the mask word of the cluster holding the voxel, {occupancy bits,
@@ -177,7 +178,6 @@ struct Hit {
 template <int STORE, bool COUNT>
 struct Ctx {
     const KScene& s;
-    const float* inv255 = nullptr;   // LDS table c / 255.0f, c in [0,255] (see load_inv255)
     const KView& v;
     uint32_t iters = 0;
     bool aborted = false;
@@ -355,9 +355,9 @@ struct Ctx {
     // (Renderer.cuh:57-86,249-258), colour packing (VoxelFunctions.cuh:69-83).
     __device__ __forceinline__ uint32_t lighting(uint32_t col, f3 n, f3 rwp, f3 ro) const {
         f3 LC = ld3(v.LC);
-        // convertRGBIntegerColorToVector: c / 255.0f per channel, read from the exact
-        // (correctly rounded) LDS table; colours are < 2^24 so R = col >> 16 <= 255.
-        f3 c = mk(inv255[col >> 16], inv255[(col >> 8) & 0xFFu], inv255[col & 0xFFu]);
+        // convertRGBIntegerColorToVector: c / 255.0f per channel, correctly rounded
+        // (div255); colours are < 2^24 so R = col >> 16 <= 255.
+        f3 c = mk(div255(col >> 16), div255((col >> 8) & 0xFFu), div255(col & 0xFFu));
         f3 r;
         if (v.use_point_light) {
             f3 p2l = sub(ld3(v.LP), add(rwp, ro));

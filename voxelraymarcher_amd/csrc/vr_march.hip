@@ -1033,14 +1033,13 @@ __device__ __forceinline__ uint32_t light_and_shadow(Walker<STORE, COUNT, CRAWL>
 // for pixel (x, local row l): colour, algorithmic bytes (+4 for the pixel write)
 // (a pixel deferred to the crawl pass comes back as 0 with 0 bytes).
 template <int STORE, int ALGO, bool COUNT, bool CRAWL>
-__device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, const float* inv255, uint32_t x, uint32_t l,
+__device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint32_t x, uint32_t l,
                                           uint32_t& bytes) {
     uint32_t col = 0;
     bytes = 0;
     f3 ro, rd;
-    if (pixel_ray<STORE == STORE_HASH>(v, x, l, ro, rd)) {
+    if (pixel_ray<true>(v, x, l, ro, rd)) {
         Walker<STORE, COUNT, CRAWL> w(s, v);
-        w.inv255 = inv255;
         Hit h;
         if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
         if (w.aborted) col = 0;
@@ -1052,11 +1051,10 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, const
 // The crawl pass's pixel: the walk a deferral record `r` left at its crawl,
 // finished from there (its iterations and bytes so far are the record's).
 template <int STORE, int ALGO, bool COUNT>
-__device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v, const float* inv255,
+__device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v,
                                                  const uint32_t* r, uint32_t& bytes) {
     const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
     Walker<STORE, COUNT, true> w(s, v);
-    w.inv255 = inv255;
     w.iters = r[9];
     w.bytes = r[10];
     const f3 o{__uint_as_float(r[2]), __uint_as_float(r[3]), __uint_as_float(r[4])};
@@ -1064,7 +1062,7 @@ __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v
     uint32_t col = 0;
     if (!(r[1] & 1u)) {                           // the primary walk crawled
         f3 ro, rd;
-        pixel_ray<STORE == STORE_HASH>(v, x, l, ro, rd);
+        pixel_ray<true>(v, x, l, ro, rd);
         Hit h;
         if (w.template primary_regions<ALGO>(o, rd, cr, h, r)) col = light_and_shadow(w, v, h);
     } else {                                      // the shadow walk crawled
@@ -1093,14 +1091,12 @@ __device__ __forceinline__ void add_bytes(const KView& v, uint32_t lane, unsigne
 #endif
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(64 * kTilesX * kTilesY, ALGO == ALGO_ORIGINAL ? VR_ORIG_WAVES : VR_LONG_WAVES) void march_kernel(KScene s, KView v) {
-    __shared__ float inv255_lds[256];
-    const float* inv255 = load_inv255(inv255_lds);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t x = (blockIdx.x * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
     const uint32_t l = (blockIdx.y * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
     uint32_t bytes = 0;
     if (x < v.W && l < v.local_rows) {
-        v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, false>(s, v, inv255, x, l, bytes);
+        v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes);
     }
     if (COUNT) add_bytes(v, lane, bytes);
 }
@@ -1109,22 +1105,20 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, ALGO == ALGO_ORIGINAL ? VR_
 // exact crawl fast-forward; the last workgroup resets the slot for reuse.
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
-    __shared__ float inv255_lds[256];
     __shared__ uint32_t n_lds;
     if (threadIdx.x == 0) n_lds = v.defer[0];
     __syncthreads();
     const uint32_t total = n_lds;
     if (total == 0u) return;                  // nothing deferred (the usual case): no reset needed
     const uint32_t n = min(total, v.defer_cap);
-    const float* inv255 = load_inv255(inv255_lds);
     unsigned long long bytes = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t* r = v.defer + 4 + (size_t)i * kDeferRecWords;
         uint32_t b;
         const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
         // an ambiguous crawl voxel (see the deferral): walk the pixel from its start
-        v.out[(size_t)l * v.W + x] = (r[1] & 4u) ? shade<STORE, ALGO, COUNT, true>(s, v, inv255, x, l, b)
-                                                 : shade_resume<STORE, ALGO, COUNT>(s, v, inv255, r, b);
+        v.out[(size_t)l * v.W + x] = (r[1] & 4u) ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b)
+                                                 : shade_resume<STORE, ALGO, COUNT>(s, v, r, b);
         bytes += b;
     }
     if (COUNT) add_bytes(v, threadIdx.x & 63u, bytes);

@@ -331,9 +331,7 @@ constexpr uint32_t kHeadStride = 64;     // one head per 256-B line
 
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(256) void persist_kernel(KScene s, KView v, uint32_t* __restrict__ queue) {
-    __shared__ float inv255_lds[256];
     Machine<STORE, ALGO, COUNT> m(s, v);
-    m.inv255 = load_inv255(inv255_lds);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t tiles_x = (v.W + 7u) / 8u;
     const uint32_t ntiles = tiles_x * ((v.local_rows + 7u) / 8u);
