@@ -37,7 +37,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-ROOT = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import voxelraymarcher_amd as vr  # noqa: E402
@@ -168,17 +168,16 @@ def main():
             lat.append(time.perf_counter() - t0)
         frame_latency_ms = float(np.median(lat)) * 1e3
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pipe.step(render)
-    pipe.drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    for rep in range(int(os.environ.get("DIAG_REPS", "4"))):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            pipe.step(render)
+        th = time.perf_counter()
+        pipe.drain()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(f"rep {rep}: {dt / args.steps * 1e3:.4f} ms/step (host enqueue {(th - t0) / args.steps * 1e3:.4f})", flush=True)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
