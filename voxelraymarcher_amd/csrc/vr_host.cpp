@@ -426,6 +426,12 @@ int make_view(const vr_scene* s, const vr_camera* cam, const vr_lighting* lit, c
         v.L[i] = lit->light_dir[i]; v.LC[i] = lit->light_color[i]; v.LP[i] = lit->light_pos[i];
         v.translation[i] = translation ? translation[i] : 0.0f;
     }
+    v.L_fast = 1u;
+    for (int i = 0; i < 3; ++i) {
+        const float a = std::fabs(v.L[i]);
+        v.Lr[i] = 1.0f / v.L[i];
+        if (!(a >= 0x1p-64f && a <= 0x1p+20f)) v.L_fast = 0u;
+    }
     v.scale_f = (float)scale;          // static_cast<float>(scale) (Ray.cuh:16)
     v.use_point_light = lit->use_point_light ? 1 : 0;
     v.use_shadows = lit->use_shadows ? 1 : 0;

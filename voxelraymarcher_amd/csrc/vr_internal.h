@@ -50,6 +50,11 @@ struct KScene {
 struct KView {
     float llc[3], hor[3], ver[3], org[3];
     float L[3], LC[3], LP[3];
+    // the light direction's reciprocals RN(1 / L_i) (host division, correctly
+    // rounded: exact in div_fast) and whether all three are in div_fast's divisor
+    // domain -- kernel arguments, so the shadow walks keep them in SGPRs
+    float Lr[3];
+    uint32_t L_fast;
     float translation[3];
     float scale_f;
     int32_t use_point_light, use_shadows;

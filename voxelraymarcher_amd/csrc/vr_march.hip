@@ -200,12 +200,11 @@ struct Walker : Ctx<STORE, COUNT> {
         float tX, tY, tZ;
         if (resume) {                             // o is the stepped position of the crawl
             tX = __uint_as_float(rs[11]); tY = __uint_as_float(rs[12]); tZ = __uint_as_float(rs[13]);
-        } else if (!CRAWL && kFastSetup) {
+        } else if (!CRAWL && rc && (kFastSetup || SHADOW)) {
             // The initial step (Renderer.cuh:269-280; shadow :106-117) with the ray's
             // hoisted reciprocals: |n| <= 1 + EPSILON here, so the fast division's
             // domain is the direction's plus |n| >= 2^-90 (see div_fast).
-            const Rcp r0x = rc ? rc[0] : rcp_setup(d.x), r0y = rc ? rc[1] : rcp_setup(d.y),
-                      r0z = rc ? rc[2] : rcp_setup(d.z);
+            const Rcp r0x = rc[0], r0y = rc[1], r0z = rc[2];
             const float sx = px ? 1.0f : -1.0f, sy = py ? 1.0f : -1.0f, sz = pz ? 1.0f : -1.0f;
             const float ax = next_plane_fma(o.x, sx, sx * kEps) - o.x, ay = next_plane_fma(o.y, sy, sy * kEps) - o.y,
                         az = next_plane_fma(o.z, sz, sz * kEps) - o.z;
@@ -260,7 +259,7 @@ struct Walker : Ctx<STORE, COUNT> {
                 // Hoisted reciprocals (div_fast) and +-1 plane signs for the loop
                 // (rcp_setup(-d) = -rcp_setup(d) bit for bit: tools/div_proof.hip).
                 Rcp rx, ry, rz;
-                if (rc && !CRAWL && kFastSetup) {
+                if (rc && !CRAWL && (kFastSetup || SHADOW)) {
                     rx = EQ ? Rcp{fabsf(dl.x), fabsf(rc[0].r), rc[0].ok} : rc[0];
                     ry = rc[1];
                     rz = rc[2];
@@ -948,7 +947,9 @@ struct Walker : Ctx<STORE, COUNT> {
     template <bool LONGEST, bool EQ = false>
     __device__ __forceinline__ bool shadow(f3 o, i3 cr, const uint32_t* rs = nullptr) {
         f3 d = ld3(v.L);
-        const Rcp rc[3] = {rcp_setup(d.x), rcp_setup(d.y), rcp_setup(d.z)};   // once per shadow ray
+        // the light's reciprocals, made on the host (uniform: SGPRs, no VGPRs)
+        const bool lf = v.L_fast != 0u;
+        const Rcp rc[3] = {Rcp{d.x, v.Lr[0], lf}, Rcp{d.y, v.Lr[1], lf}, Rcp{d.z, v.Lr[2], lf}};
         Hit dummy;
         if (CRAWL && rs != nullptr) {            // resume a deferred crawl (as primary_regions)
             const bool hit = grid_original_rt(o, d, this->region_at_nocount(cr), cr, dummy, true, EQ, rs);
