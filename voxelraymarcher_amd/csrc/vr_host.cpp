@@ -844,6 +844,7 @@ int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr
     v.row0 = opts->row_begin;
     v.row_limit = opts->row_end;
     v.band_rows = band;
+    v.band_minv = band == 1u ? 0xFFFFFFFFu : (uint32_t)((1ull << 32) / band);
     v.rank = opts->rank;
     v.nranks = opts->nranks;
     v.local_rows = (uint32_t)(vr_band_buffer_words(width, rows, band, opts->nranks) / width);

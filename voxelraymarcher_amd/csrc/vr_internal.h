@@ -60,6 +60,7 @@ struct KView {
     int32_t use_point_light, use_shadows;
     uint32_t W, H;
     uint32_t row0, band_rows, rank, nranks, local_rows, row_limit;
+    uint32_t band_minv;       // floor(2^32 / band_rows) (2^32 - 1 for 1): l / band_rows by a multiply-high
     uint32_t* out;
     unsigned long long* bytes;
     uint32_t* defer;          // crawl deferral slot: [count, done, 0, 0, records (kDeferRecWords each)...]

@@ -878,8 +878,8 @@ struct Walker : Ctx<STORE, COUNT> {
         f3 tr = ld3(v.translation);
         f3 so = scl(v.scale_f, sub(wo, tr));      // Ray::convertRayToLocalSpace (Ray.cuh:14-17)
         f3 d = wd;
-        // the ray's reciprocals, made once for every division by d (div_fast; cuckoo
-        // store only, see kFastSetup)
+        // the ray's reciprocals, made once for every division by d in the entry clip
+        // (div_fast) and, cuckoo store only (see kFastSetup), in the region walks
         const Rcp rc[3] = {rcp_setup(d.x), rcp_setup(d.y), rcp_setup(d.z)};
         i3 cr{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
         VR_DIAG_COUNT(14);                            // primary() calls
@@ -892,11 +892,10 @@ struct Walker : Ctx<STORE, COUNT> {
                         az = (float)(nz * kBlock) - so.z;
             float tX = div_fast(ax, rc[0]), tY = div_fast(ay, rc[1]), tZ = div_fast(az, rc[2]);
             // (a numerator is never -0 here; +0 divides exactly)
-            const bool fast = kFastSetup &&
-                              (__float_as_uint(ax) == 0u || div_fast_ok(ax, rc[0])) &&
+            const bool fast = (__float_as_uint(ax) == 0u || div_fast_ok(ax, rc[0])) &&
                               (__float_as_uint(ay) == 0u || div_fast_ok(ay, rc[1])) &&
                               (__float_as_uint(az) == 0u || div_fast_ok(az, rc[2]));
-            if (!kFastSetup || __builtin_expect(__builtin_amdgcn_ballot_w64(!fast) != 0, 0)) {
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(!fast) != 0, 0)) {
                 tX = fast ? tX : ax / d.x;
                 tY = fast ? tY : ay / d.y;
                 tZ = fast ? tZ : az / d.z;
@@ -982,8 +981,11 @@ struct Walker : Ctx<STORE, COUNT> {
 // FAST (cuckoo store, see Walker::kFastSetup): divisions with hoisted reciprocals.
 template <bool FAST>
 __device__ __forceinline__ bool pixel_ray(const KView& v, uint32_t x, uint32_t l, f3& ro, f3& rd) {
-    const uint32_t band = l / v.band_rows;
-    const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + (l - band * v.band_rows);
+    // band = l / band_rows: q0 = mulhi(l, floor(2^32 / band_rows)) is q or q - 1 (see FastMod)
+    const uint32_t q0 = __umulhi(l, v.band_minv), r0 = l - q0 * v.band_rows;
+    const bool up = r0 >= v.band_rows;
+    const uint32_t band = q0 + (up ? 1u : 0u), in_band = up ? r0 - v.band_rows : r0;
+    const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + in_band;
     if (y >= v.row_limit) return false;
     if (!FAST) {
         float u = ((float)x + 0.5f) / (float)v.W;
