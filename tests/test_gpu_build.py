@@ -73,6 +73,23 @@ def test_device_build_errors():
     assert e.value.code == -1
 
 
+@pytest.mark.parametrize("build", [vr.Build.DEVICE, vr.Build.HOST], ids=["device", "host"])
+def test_vcs_region_limit(build):
+    """VCS walks address cluster masks by a 32-bit byte offset (64 KB per occupied
+    region): a VCS scene may hold at most 65 536 occupied regions; more is an error,
+    the hash store has no such limit."""
+    g = np.arange(41, dtype=np.int32) * 64
+    xyz = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)   # 68 921 regions
+    rgb = np.full(len(xyz), 7, np.uint32)
+    with pytest.raises(vr.VrError) as e:
+        vr.create_scene(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE, build=build)
+    assert e.value.code == -1 and "65536" in str(e.value)
+    if build == vr.Build.DEVICE:            # the largest allowed scene (4 GB of masks) builds
+        ok = vr.create_scene(xyz[:65536], rgb[:65536], vr.StorageType.VOXEL_CLUSTER_STORE, build=build)
+        assert ok.info()["region_count"] == 65536
+        ok.close()
+
+
 def test_device_built_scene_renders_like_oracle():
     """End to end: a scene built on the GPU renders bit-exactly (C1 frame, both stores)."""
     import oracle

@@ -372,6 +372,11 @@ int build_scene_gpu(int store, const int32_t* xyz, const uint32_t* rgb, uint64_t
     }
     out.n_regions = nr;
     out.n_voxels = m;
+    if (store == STORE_VCS && nr > kVcsMaxRegions) {
+        err = "VCS scene with " + std::to_string(nr) + " occupied 64^3 regions (at most " +
+              std::to_string(kVcsMaxRegions) + ")";
+        return -1;
+    }
 
     if (store == STORE_VCS) {
         const uint64_t words = std::max<uint64_t>((uint64_t)nr * 8192u, 16u);

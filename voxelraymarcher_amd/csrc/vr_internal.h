@@ -16,6 +16,10 @@ constexpr uint32_t kEmpty = 1u << 30;        // EMPTY_KEY == EMPTY_VAL (VoxelFun
 constexpr uint32_t kNone = 0xFFFFFFFFu;      // null region / null cluster in the tables
 constexpr int32_t kBlock = 64;               // BLOCK_SIZE (VoxelFunctions.cuh:24)
 constexpr uint32_t kIterBudget = 65536u;     // per-pixel hang guard
+// VCS walks address a region's cluster masks as a 32-bit byte offset from the
+// scene's mask array (64 KB per occupied 64^3 region): at most 65536 occupied
+// regions (4 GB of masks) per VCS scene; the builders reject larger scenes.
+constexpr uint32_t kVcsMaxRegions = 65536u;
 
 // Device view of one immutable scene.  All offsets are 32-bit word indices.
 //  region_slot[D^3]          : region index r, or kNone (null StorageStructure*)

@@ -232,6 +232,9 @@ struct Walker : Ctx<STORE, COUNT> {
             // word index is a few bit operations and the lookup needs no
             // range check (Ctx::lookup's general form handles the rest).
             const uint2* mreg = s.vcs_mask + (size_t)reg * 8192u;
+            // the region's mask words as a 32-bit byte offset from the scene's (uniform)
+            // mask array: the loads take the SGPR-base form (one VGPR, no 64-bit add)
+            const uint32_t moff = reg << 16;
             // Straight-line body with one exit: the hit test, the region test of
             // the stepped position and the iteration budget are folded into a
             // single condition; the step of the hit iteration is computed and
@@ -299,7 +302,8 @@ struct Walker : Ctx<STORE, COUNT> {
                             const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
                             this->count(4);
                             const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
-                            blk = mreg[wi];
+                            blk = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) +
+                                                                  (moff | (wi << 3)));
                             __builtin_amdgcn_sched_barrier(0);   // issue the load before the planes
                             // both candidate planes, computed while the mask word is in
                             // flight and materialised (with the whole 8-B word: one load)
@@ -737,6 +741,10 @@ struct Walker : Ctx<STORE, COUNT> {
         const bool mid_floor = comp(ds, M) < 0.0f;   // decimalToIntFunc (:784)
         const float dsM = comp(ds, M), dsS = comp(ds, S), dsL = comp(ds, L);
         const uint2* mreg = s.vcs_mask + (size_t)reg * 8192u;
+        const uint32_t moff = reg << 16;              // SGPR-base loads (see grid_original_rt)
+        auto mload = [&](uint32_t w) {
+            return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) + (moff | (w << 3)));
+        };
         float tX = 0.0f, tY = 0.0f, tZ = 0.0f, tMin = 0.0f;   // the jump's last skip (hit normal)
         bool jumping = false;
         for (;;) {
@@ -789,8 +797,8 @@ struct Walker : Ctx<STORE, COUNT> {
             const uint32_t w0 = this->word_index((uint32_t)p0.x & 63u, (uint32_t)p0.y & 63u, (uint32_t)p0.z & 63u);
             const uint32_t w1 = this->word_index((uint32_t)p1.x & 63u, (uint32_t)p1.y & 63u, (uint32_t)p1.z & 63u);
             const uint32_t w2 = this->word_index((uint32_t)p2.x & 63u, (uint32_t)p2.y & 63u, (uint32_t)p2.z & 63u);
-            Blk b0 = mreg[w0], b1 = mreg[w1];
-            const Blk b2 = mreg[w2];
+            Blk b0 = mload(w0), b1 = mload(w1);
+            const Blk b2 = mload(w2);
             if (__builtin_expect(__builtin_amdgcn_ballot_w64(!inr) != 0, 0)) {
                 if (!inr) {       // huge grid coordinates: the general (aliasing) form
                     b0 = this->mask_word(reg, p0.x, p0.y, p0.z);
