@@ -297,7 +297,6 @@ struct Walker : Ctx<STORE, COUNT> {
                         uint32_t ic = this->iters + (0x42800000u - kIterBudget);
                         VR_DIAG_COUNT((SHADOW ? 4 : 0) + (SX == 0 ? 1 : 0));   // walk entries
                         for (;;) {
-                            ++ic;
                             VR_DIAG_COUNT((SHADOW ? 6 : 2) + (SX == 0 ? 1 : 0));   // loop iterations
                             const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
                             this->count(4);
@@ -334,7 +333,7 @@ struct Walker : Ctx<STORE, COUNT> {
                                 if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
                                     sMin = bad ? am / fabsf(d.x) : sMin;
                                     crawl = bad & walk_ok & skip & (sMin == 0.0f) &
-                                            (CRAWL ? ic - (0x42800000u - kIterBudget) >= crawl_after : !crawl_off);
+                                            (CRAWL ? ic + 1u - (0x42800000u - kIterBudget) >= crawl_after : !crawl_off);
                                     if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
                                 }
                             } else {
@@ -347,7 +346,7 @@ struct Walker : Ctx<STORE, COUNT> {
                                     // a skip step with t = 0 (its plane axis has n = 0, so it is
                                     // always on this branch): the ray creeps through an empty cluster
                                     crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
-                                            (CRAWL ? ic - (0x42800000u - kIterBudget) >= crawl_after : !crawl_off);
+                                            (CRAWL ? ic + 1u - (0x42800000u - kIterBudget) >= crawl_after : !crawl_off);
                                     if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
                                 }
                                 sMin = fminf(sX, fminf(sY, sZ));
@@ -360,6 +359,8 @@ struct Walker : Ctx<STORE, COUNT> {
                             o = EQ ? add(o, f3{ts * d.x, ts * d.x, ts * d.x}) : add(o, scl(ts, d));
                             // One unsigned compare for hit, region exit (in_region_bits_nz of the
                             // stepped position) and the budget (iters >= kIterBudget):
+                            // (the add as asm: loop strength reduction otherwise keeps two counters)
+                            asm("v_add_u32 %0, 1, %0" : "+v"(ic));
                             const uint32_t ev = max(max(max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)),
                                                         ic), fm);
                             if (ev >= 0x42800000u || crawl) break;
@@ -492,7 +493,6 @@ struct Walker : Ctx<STORE, COUNT> {
             uint2 e1{0u, 0u}, e2{0u, 0u};
             uint32_t ic = this->iters + (0x42800000u - kIterBudget);   // biased count (see the VCS walk)
             for (;;) {
-                ++ic;
                 const uint32_t vx = (uint32_t)f2i(o.x), vy = (uint32_t)f2i(o.y), vz = (uint32_t)f2i(o.z);
                 key = lshl_or(lshl_or(vx, 10u, vy), 10u, vz);              // generate3DPoint (x<<20|y<<10|z)
                 e1 = t1[fastmod(hash1(key, m.w), fmod)];
@@ -527,6 +527,7 @@ struct Walker : Ctx<STORE, COUNT> {
                 // a hit keeps o unstepped: step length (-EPSILON) + EPSILON = +0 (see the VCS walk)
                 const float ts = bit_select(fm, -kEps, sMin) + kEps;
                 o = EQ ? add(o, f3{ts * d.x, ts * d.x, ts * d.x}) : add(o, scl(ts, d));
+                asm("v_add_u32 %0, 1, %0" : "+v"(ic));      // (see the VCS walk)
                 const uint32_t ev = max(max(max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)), ic), fm);
                 if (ev >= 0x42800000u) break;
             }
