@@ -81,7 +81,8 @@ struct KView {
 //   2-4 stepped position      5-7 region         8 unused (0)
 //   9 iterations so far       10 counted bytes so far
 //   11-13 tX, tY, tZ of the last voxel step (hit normal; 0 for shadow walks)
-//   14 reserved (0)           15-17 the crawl iteration's voxel   18 lit colour   19 unused
+//   14 reserved (0)           15-17 the crawl iteration's voxel (filled in by the crawl pass)
+//   18 lit colour             19 unused
 // A slot is used by one launch at a time (vr_host.cpp SlotRing).
 constexpr uint32_t kDeferCap = 16384;
 constexpr uint32_t kDeferRecWords = 20;

@@ -200,11 +200,14 @@ struct Walker : Ctx<STORE, COUNT> {
         float tX, tY, tZ;
         if (resume) {                             // o is the stepped position of the crawl
             tX = __uint_as_float(rs[11]); tY = __uint_as_float(rs[12]); tZ = __uint_as_float(rs[13]);
-        } else if (!CRAWL && rc && (kFastSetup || SHADOW)) {
+        } else if (!CRAWL) {
             // The initial step (Renderer.cuh:269-280; shadow :106-117) with the ray's
-            // hoisted reciprocals: |n| <= 1 + EPSILON here, so the fast division's
-            // domain is the direction's plus |n| >= 2^-90 (see div_fast).
-            const Rcp r0x = rc[0], r0y = rc[1], r0z = rc[2];
+            // hoisted reciprocals (or the walk's own, which its loop shares): |n| <= 1 +
+            // EPSILON here, so the fast division's domain is the direction's plus
+            // |n| >= 2^-90 (see div_fast).
+            const bool use_rc = rc && (kFastSetup || SHADOW);
+            const Rcp r0x = use_rc ? rc[0] : rcp_setup(d.x), r0y = use_rc ? rc[1] : rcp_setup(d.y),
+                      r0z = use_rc ? rc[2] : rcp_setup(d.z);
             const float sx = px ? 1.0f : -1.0f, sy = py ? 1.0f : -1.0f, sz = pz ? 1.0f : -1.0f;
             const float ax = next_plane_fma(o.x, sx, sx * kEps) - o.x, ay = next_plane_fma(o.y, sy, sy * kEps) - o.y,
                         az = next_plane_fma(o.z, sz, sz * kEps) - o.z;
@@ -368,22 +371,34 @@ struct Walker : Ctx<STORE, COUNT> {
                         this->iters = ic - (0x42800000u - kIterBudget);
                     };
                     const uint32_t sg = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
-                    const uint32_t sg0 = __builtin_amdgcn_readfirstlane(sg);
                     using N = Sgn<-1>;
                     using P = Sgn<1>;
-                    if (!CRAWL && __builtin_amdgcn_ballot_w64(sg != sg0) == 0 && (!EQ || sg0 == 0u || sg0 == 7u)) {
-                        switch (sg0) {
-                        case 0: walk(N{}, N{}, N{}); break;
-                        case 7: walk(P{}, P{}, P{}); break;
-                        case 1: if (!EQ) walk(P{}, N{}, N{}); break;
-                        case 2: if (!EQ) walk(N{}, P{}, N{}); break;
-                        case 3: if (!EQ) walk(P{}, P{}, N{}); break;
-                        case 4: if (!EQ) walk(N{}, N{}, P{}); break;
-                        case 5: if (!EQ) walk(P{}, N{}, P{}); break;
-                        default: if (!EQ) walk(N{}, P{}, P{}); break;
-                        }
-                    } else {
+                    if (CRAWL) {
                         walk(Sgn<0>{}, Sgn<0>{}, Sgn<0>{});
+                    } else {
+                        // One pass of the loop specialised for each sign pattern present in
+                        // the wave (nearly always one; a tile straddling a plane where a
+                        // direction component changes sign runs two or more, one after the
+                        // other).  A generic, per-lane-sign loop in this kernel needed ~81
+                        // VGPRs against the specialised loops' ~72 (7 waves/SIMD).  (An
+                        // equal-component shadow direction has pattern 0 or 7.)
+                        bool todo = true;
+                        while (todo) {
+                            const uint32_t pat = __builtin_amdgcn_readfirstlane(sg);
+                            if (sg == pat) {
+                                todo = false;
+                                switch (pat) {
+                                case 0: walk(N{}, N{}, N{}); break;
+                                case 7: walk(P{}, P{}, P{}); break;
+                                case 1: if (!EQ) walk(P{}, N{}, N{}); break;
+                                case 2: if (!EQ) walk(N{}, P{}, N{}); break;
+                                case 3: if (!EQ) walk(P{}, P{}, N{}); break;
+                                case 4: if (!EQ) walk(N{}, N{}, P{}); break;
+                                case 5: if (!EQ) walk(P{}, N{}, P{}); break;
+                                default: if (!EQ) walk(N{}, P{}, P{}); break;
+                                }
+                            }
+                        }
                     }
                 }
                 // Why the lane left, recomputed from values the loop keeps in VGPRs
@@ -425,19 +440,9 @@ struct Walker : Ctx<STORE, COUNT> {
                             // (a shadow walk has no normal: its t values are not kept live for this)
                             r[11] = SHADOW ? 0u : __float_as_uint(tX); r[12] = SHADOW ? 0u : __float_as_uint(tY);
                             r[13] = SHADOW ? 0u : __float_as_uint(tZ); r[14] = 0u;   // reserved
-                            // The crawl iteration's voxel q (see crawl_voxel): recovered from
-                            // the stepped position; if it cannot be, the crawl pass walks the
-                            // pixel from its start instead.
-                            bool amb = false;
-                            uint32_t qq[3];
-#pragma unroll 1
-                            for (uint32_t a = 0; a < 3u; ++a) {
-                                int32_t qa;
-                                amb |= !crawl_voxel(comp(o, a), kEps * comp(d, a), qa);
-                                qq[a] = (uint32_t)qa;
-                            }
-                            r[1] |= (amb || v.crawl_rewalk) ? 4u : 0u;
-                            r[15] = qq[0]; r[16] = qq[1]; r[17] = qq[2];
+                            // (the crawl iteration's voxel q, words 15-17, is recovered from the
+                            // stepped position by the crawl pass: see crawl_kernel)
+                            r[1] |= v.crawl_rewalk ? 4u : 0u;
                             r[18] = this->lit_saved;
                             if (COUNT) this->bytes = 0xFFFFFFFCu;     // + the final 4 = 0
                             aborted = true;
@@ -1125,12 +1130,30 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     const uint32_t n = min(total, v.defer_cap);
     unsigned long long bytes = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t* r = v.defer + 4 + (size_t)i * kDeferRecWords;
+        uint32_t* r = v.defer + 4 + (size_t)i * kDeferRecWords;
         uint32_t b;
         const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
-        // an ambiguous crawl voxel (see the deferral): walk the pixel from its start
-        v.out[(size_t)l * v.W + x] = (r[1] & 4u) ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b)
-                                                 : shade_resume<STORE, ALGO, COUNT>(s, v, r, b);
+        // The crawl iteration's voxel q (see crawl_voxel), recovered from the stepped
+        // position and the walk's direction (the pixel's ray, or the light for a shadow
+        // walk) into record words 15-17; if it cannot be, the pixel is walked from its
+        // start (as for every record under VR_KERNEL_TILE_REWALK, flag 4).
+        bool amb = (r[1] & 4u) != 0u;
+        if (!amb) {
+            f3 d = ld3(v.L);
+            if (!(r[1] & 1u)) {
+                f3 ro;
+                pixel_ray<true>(v, x, l, ro, d);
+            }
+            const f3 o{__uint_as_float(r[2]), __uint_as_float(r[3]), __uint_as_float(r[4])};
+#pragma unroll 1
+            for (uint32_t a = 0; a < 3u; ++a) {
+                int32_t qa;
+                amb |= !crawl_voxel(comp(o, a), kEps * comp(d, a), qa);
+                r[15 + a] = (uint32_t)qa;
+            }
+        }
+        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b)
+                                         : shade_resume<STORE, ALGO, COUNT>(s, v, r, b);
         bytes += b;
     }
     if (COUNT) add_bytes(v, threadIdx.x & 63u, bytes);
