@@ -294,6 +294,13 @@ struct Walker : Ctx<STORE, COUNT> {
                     // then need no sign multiplications (see plane_v / plane_c8).
                     auto walk = [&](auto SXc, auto SYc, auto SZc) {
                         constexpr int SX = decltype(SXc)::value, SY = decltype(SYc)::value, SZ = decltype(SZc)::value;
+                        // All three components positive (every lane of this pass, and every
+                        // lane's reciprocals in div_fast's domain: checked before this loop is
+                        // chosen): then no numerator is ever tiny or zero -- a voxel plane lies
+                        // >= ~EPSILON/2 beyond o, a cluster plane (v & ~7) + 8 > o by >= ulp(64)
+                        // -- so the division needs no fallback, and no crawl (t = 0) can occur.
+                        // (Sgn<2>: positive, and the caller checked the reciprocals)
+                        constexpr bool kPos = SX == 2 && SY == 2 && SZ == 2;
                         // The iteration count as the budget test reads it, biased so that
                         // it reaches bits(64.0f) exactly when iters exceeds kIterBudget:
                         // one add per iteration.
@@ -332,8 +339,8 @@ struct Walker : Ctx<STORE, COUNT> {
                                 // a = +0, d < 0), which neither the step nor the crawl test sees
                                 const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
                                 sMin = div_fast(am, rx);
-                                const bool bad = !(am >= nlim);
-                                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                                const bool bad = !kPos && !(am >= nlim);
+                                if (!kPos && __builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
                                     sMin = bad ? am / fabsf(d.x) : sMin;
                                     crawl = bad & walk_ok & skip & (sMin == 0.0f) &
                                             (CRAWL ? ic + 1u - (0x42800000u - kIterBudget) >= crawl_after : !crawl_off);
@@ -341,8 +348,8 @@ struct Walker : Ctx<STORE, COUNT> {
                                 }
                             } else {
                                 float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
-                                const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
-                                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                                const bool bad = !kPos && !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
+                                if (!kPos && __builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
                                     sX = bad ? (zx ? kInf : ax / d.x) : sX;
                                     sY = bad ? (zy ? kInf : ay / d.y) : sY;
                                     sZ = bad ? (zz ? kInf : az / d.z) : sZ;
@@ -389,7 +396,10 @@ struct Walker : Ctx<STORE, COUNT> {
                                 todo = false;
                                 switch (pat) {
                                 case 0: walk(N{}, N{}, N{}); break;
-                                case 7: walk(P{}, P{}, P{}); break;
+                                case 7:
+                                    if (__builtin_amdgcn_ballot_w64(!walk_ok) == 0) walk(Sgn<2>{}, Sgn<2>{}, Sgn<2>{});
+                                    else walk(P{}, P{}, P{});
+                                    break;
                                 case 1: if (!EQ) walk(P{}, N{}, N{}); break;
                                 case 2: if (!EQ) walk(N{}, P{}, N{}); break;
                                 case 3: if (!EQ) walk(P{}, P{}, N{}); break;
