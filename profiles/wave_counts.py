@@ -22,7 +22,9 @@ NAMES = {0: "primary VCS walks (sign-specialised)", 1: "primary VCS walks (gener
          8: "grid_original calls (primary)", 9: "grid_original calls (shadow)",
          10: "primary region rounds", 11: "primary null-region skips", 12: "shadow region rounds",
          13: "shadow null-region skips", 14: "primary() calls", 15: "entry-clip iterations",
-         16: "shadow walks started"}
+         16: "shadow walks started", 17: "primary longest-axis walks", 18: "primary longest-axis iterations",
+         19: "shadow longest-axis walks", 20: "shadow longest-axis iterations",
+         21: "longest-axis iterations with a jumping lane"}
 
 name = sys.argv[1] if len(sys.argv) > 1 else "C2"
 cfg = vr.CONFIGS[name]

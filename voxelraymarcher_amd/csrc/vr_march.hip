@@ -27,8 +27,13 @@ __device__ unsigned long long g_vr_diag[32];
         if (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) \
             atomicAdd(&g_vr_diag[(k)], 1ull);                                        \
     } while (0)
+#define VR_DIAG_COUNT_IF(c, k)                                  \
+    do {                                                       \
+        if (__builtin_amdgcn_ballot_w64(c) != 0) VR_DIAG_COUNT(k); \
+    } while (0)
 #else
 #define VR_DIAG_COUNT(k) do { } while (0)
+#define VR_DIAG_COUNT_IF(c, k) do { } while (0)
 #endif
 
 namespace vr {
@@ -716,184 +721,273 @@ struct Walker : Ctx<STORE, COUNT> {
 
     // The VCS longest-axis walk with ONE reference loop iteration per loop
     // iteration (rayMarchVoxelGridLongestAxis, Renderer.cuh:760-915; shadow twin
-    // :495-631; performVoxelSpaceJump :696-751 / :441-492).  A lane is either
-    //   main : one whole iteration of the reference's while loop -- its (up to
-    //          three) axis probes are known at its top (M/S in crossing order, then
-    //          L, each adding one axis of `ad` to the grid position), so their three
-    //          mask words are loaded together and evaluated in order; the first
-    //          absent cluster starts a jump, the first stored voxel is the hit, or
+    // :495-631; performVoxelSpaceJump :696-751 / :441-492), specialised on the
+    // ray's axis order: L, M, S (longest, middle, shortest) are compile-time, so
+    // the walk state lives in (L, M, S) registers and no axis is selected at run
+    // time (a wave runs one pass per order its lanes hold; shadow rays share one).
+    // A lane is either
+    //   main : one whole iteration of the reference's while loop -- its probes
+    //          are known at its top: slot A (the first crossing, M or S), slot B
+    //          (both crossings) and slot C (g + ad, the L step); their three mask
+    //          words are loaded together and evaluated in order; the first absent
+    //          cluster starts a jump, the first stored voxel is the hit, or
     //   jump : one cluster skip of performVoxelSpaceJump and the probe of the
-    //          cell it lands in (the jump's first existence test re-reads the
-    //          probe that started it, known absent: counted, not loaded).
+    //          cell it lands in (slot C; the jump's first existence test re-reads
+    //          the probe that started it, known absent: counted, not loaded).
     // Probes, ticks and counted bytes are the reference's, in its order; the
     // later probes of an iteration that stops early are loaded but not counted.
-    template <bool SHADOW>
-    __device__ __forceinline__ bool grid_longest_vcs(f3& oo, f3 od, uint32_t reg, i3 cr, Hit& h) {
-        uint32_t L, M, S;
+    // Returns the hit; `tail` = the loop ended in the region (the caller runs
+    // the original DDA from oo, Renderer.cuh:912-914, once for every order).
+    template <int A>
+    __device__ __forceinline__ static float ax3(f3 v) { return A == 0 ? v.x : (A == 1 ? v.y : v.z); }
+    template <bool SHADOW, int PL, int PM, int PS>
+    __device__ __forceinline__ bool walk_longest_vcs(f3& oo, f3 od, uint32_t reg, bool& tail, uint32_t& hcol,
+                                                     uint32_t& hcode) {
         // Ray::convertRayToLongestAxisDirection (Ray.cuh:19-71)
-        float ax = fabsf(od.x), ay = fabsf(od.y), az = fabsf(od.z), k;
-        if (ax > ay && ax > az) {
-            L = 0; M = ay > az ? 1 : 2; S = ay > az ? 2 : 1; k = 1.0f / ax;
-        } else if (ay > az) {
-            L = 1; M = ax > az ? 0 : 2; S = ax > az ? 2 : 0; k = 1.0f / ay;
-        } else {
-            L = 2; M = ax > ay ? 0 : 1; S = ax > ay ? 1 : 0; k = 1.0f / az;
-        }
-        const f3 ds = scl(k, od);
-        f3 old_o = oo;
-        i3 g{f2i(oo.x), f2i(oo.y), f2i(oo.z)};
-        i3 ad{0, 0, 0};
-        const int32_t adL = comp(od, L) < 0.0f ? -1 : 1;
-        seti(ad, L, adL);
-        f3 ray_o;
+        const float odL = ax3<PL>(od), odM = ax3<PM>(od), odS = ax3<PS>(od);
+        const float k = 1.0f / fabsf(odL);
+        const float dL = k * odL, dM = k * odM, dS = k * odS;
+        // walk frame <-> grid axes (x, y, z): constant indices, registers only
+        auto xyz = [](auto l, auto m, auto s) {
+            struct { decltype(l) c[3]; } r;
+            r.c[PL] = l; r.c[PM] = m; r.c[PS] = s;
+            return r;
+        };
+        auto to_f3 = [&](float l, float m, float s) {
+            const auto c = xyz(l, m, s);
+            return mk(c.c[0], c.c[1], c.c[2]);
+        };
+        auto to_i3 = [&](int32_t l, int32_t m, int32_t s) {
+            const auto c = xyz(l, m, s);
+            return i3{c.c[0], c.c[1], c.c[2]};
+        };
+        auto word = [&](int32_t l, int32_t m, int32_t s) {
+            const auto c = xyz((uint32_t)l & 63u, (uint32_t)m & 63u, (uint32_t)s & 63u);
+            return this->word_index(c.c[0], c.c[1], c.c[2]);
+        };
+        auto bit5 = [&](int32_t l, int32_t m, int32_t s) {
+            const auto c = xyz((uint32_t)l, (uint32_t)m, (uint32_t)s);
+            return this->word_bit5(c.c[1], c.c[2]) & 31u;
+        };
+        float oL = ax3<PL>(oo), oM = ax3<PM>(oo), oS = ax3<PS>(oo);      // oldRay origin
+        int32_t gL = f2i(oL), gM = f2i(oM), gS = f2i(oS);                 // gridValues
+        const int32_t aL = odL < 0.0f ? -1 : 1;                           // axisDiff[L]
+        float rL, rM, rS;                                                 // ray origin
         {
-            // x / (float)adL with adL = +-1 is exactly x * adL
-            const float gL = (float)geti(g, L), oL = comp(oo, L);
-            const float t = adL > 0 ? (gL + kEps + 1.0f - oL) * (float)adL : (gL - kEps - oL) * (float)adL;
-            ray_o = add(old_o, scl(t, ds));
+            // x / (float)aL with aL = +-1 is exactly x * aL
+            const float t = aL > 0 ? ((float)gL + kEps + 1.0f - oL) * (float)aL : ((float)gL - kEps - oL) * (float)aL;
+            rL = oL + t * dL; rM = oM + t * dM; rS = oS + t * dS;
         }
-        seti(ad, M, f2i(comp(ray_o, M)) - geti(g, M));
-        seti(ad, S, f2i(comp(ray_o, S)) - geti(g, S));
-        const bool mid_floor = comp(ds, M) < 0.0f;   // decimalToIntFunc (:784)
-        const float dsM = comp(ds, M), dsS = comp(ds, S), dsL = comp(ds, L);
-        const uint2* mreg = s.vcs_mask + (size_t)reg * 8192u;
+        int32_t aM = f2i(rM) - gM, aS = f2i(rS) - gS;
+        const bool mid_floor = dM < 0.0f;                                 // decimalToIntFunc (:784)
+        // the walk's reciprocals: its divisions by dL, dM, dS are div_fast (IEEE
+        // fallback off the domain)
+        const Rcp qL = rcp_setup(dL), qM = rcp_setup(dM), qS = rcp_setup(dS);
+        const bool qok = qL.ok && qM.ok && qS.ok;
         const uint32_t moff = reg << 16;              // SGPR-base loads (see grid_original_rt)
         auto mload = [&](uint32_t w) {
             return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) + (moff | (w << 3)));
         };
-        float tX = 0.0f, tY = 0.0f, tZ = 0.0f, tMin = 0.0f;   // the jump's last skip (hit normal)
+        uint32_t nj = 0;                  // the jump's last skip: getNormalFromTValues' axis (x, y, z)
         bool jumping = false;
+        uint32_t exitk = 0, stop = 3u, col = 0;   // loop exit: 0 = tail, 1 = hit, 2 = left the region
+        bool mfirst = false;
+        VR_DIAG_COUNT(SHADOW ? 19 : 17);               // longest-axis walks
         for (;;) {
-            // ---- the probes of this iteration: slots 0..n-1 (slot n-1 of a main lane is g + ad)
-            i3 p0, p1, p2;
-            uint32_t n, a0 = L, a1 = L;
+            VR_DIAG_COUNT(SHADOW ? 20 : 18);           // longest-axis loop iterations
+            VR_DIAG_COUNT_IF(jumping, 21);             // ... with a jumping lane
+            // ---- this iteration's probe slots (A.L = B.L = gL)
+            int32_t AM, AS, CL, CM, CS;
+            bool vA = false, vB = false;
+            mfirst = false;
             if (!jumping) {
-                p2 = i3{g.x + ad.x, g.y + ad.y, g.z + ad.z};
-                if (!grid_in_region(p2.x, p2.y, p2.z)) break;          // -> the original-DDA tail
+                CL = gL + aL; CM = gM + aM; CS = gS + aS;
+                if (!grid_in_region(CL, CM, CS)) break;   // exitk 0: the original-DDA tail
                 if (!tick()) return false;
-                const int32_t adM = geti(ad, M), adS = geti(ad, S);
-                if (adS != 0 && adM != 0) {
-                    const float om = comp(old_o, M);
-                    const float t1 = ((mid_floor ? floorf(om) : ceilf(om)) - om) / dsM;
-                    const float sp = comp(old_o, S) + dsS * t1;
-                    const int32_t sd = f2i(floorf(sp)) - geti(g, S);
-                    a0 = sd != 0 ? S : M;
-                    a1 = sd != 0 ? M : S;
-                    n = 3;
-                } else {
-                    a0 = adM != 0 ? M : S;
-                    n = (adM | adS) != 0 ? 2u : 1u;
+                const bool hasM = aM != 0, hasS = aS != 0;
+                bool sfirst = false;
+                if (hasM && hasS) {
+                    // (the numerator is +0 or in (-1, 1): div_fast's domain is |n| >= 2^-90)
+                    const float n1 = (mid_floor ? floorf(oM) : ceilf(oM)) - oM;
+                    float t1 = div_fast(n1, qM);
+                    const bool bad = !(qM.ok && (n1 == 0.0f || fabsf(n1) >= 0x1p-90f));
+                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) t1 = bad ? n1 / dM : t1;
+                    const float sp = oS + dS * t1;
+                    sfirst = f2i(floorf(sp)) - gS != 0;
                 }
-                p0 = g; seti(p0, a0, geti(g, a0) + geti(ad, a0));
-                p1 = p0; seti(p1, a1, geti(p0, a1) + geti(ad, a1));
-                if (n == 2u) { p1 = p2; a1 = L; }
-                if (n == 1u) { p0 = p2; a0 = L; }
+                vA = hasM || hasS;
+                vB = hasM && hasS;
+                mfirst = hasM && !sfirst;
+                AM = mfirst ? CM : gM;
+                AS = mfirst ? gS : CS;
             } else {
                 if (!tick()) return false;
                 // performVoxelSpaceJump's cluster skip (:707-725), integer planes from g
-                const int32_t nx = ds.x > 0.0f ? ((g.x / 8) + 1) * 8 : (g.x / 8) * 8;
-                const int32_t ny = ds.y > 0.0f ? ((g.y / 8) + 1) * 8 : (g.y / 8) * 8;
-                const int32_t nz = ds.z > 0.0f ? ((g.z / 8) + 1) * 8 : (g.z / 8) * 8;
-                tX = ((float)nx - old_o.x) / ds.x;
-                tY = ((float)ny - old_o.y) / ds.y;
-                tZ = ((float)nz - old_o.z) / ds.z;
-                tMin = fminf(tX, fminf(tY, tZ)) + kEps;
-                old_o = add(old_o, scl(tMin, ds));
-                g = i3{f2i(floorf(old_o.x)), f2i(floorf(old_o.y)), f2i(floorf(old_o.z))};
-                if (!grid_in_region(g.x, g.y, g.z)) {
-                    oo = old_o;
-                    return false;
+                const int32_t nL = dL > 0.0f ? ((gL / 8) + 1) * 8 : (gL / 8) * 8;
+                const int32_t nM = dM > 0.0f ? ((gM / 8) + 1) * 8 : (gM / 8) * 8;
+                const int32_t nS = dS > 0.0f ? ((gS / 8) + 1) * 8 : (gS / 8) * 8;
+                const float nl = (float)nL - oL, nm = (float)nM - oM, ns = (float)nS - oS;
+                float tl = div_fast(nl, qL), tm = div_fast(nm, qM), ts = div_fast(ns, qS);
+                // (numerators of in-region cells are < 73; +0 divides exactly but takes the
+                // IEEE branch here, rarely)
+                const bool bad = !(qok && fminf(fabsf(nl), fminf(fabsf(nm), fabsf(ns))) >= 0x1p-90f &&
+                                   fmaxf(fabsf(nl), fmaxf(fabsf(nm), fabsf(ns))) <= 0x1p+20f);
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                    tl = bad ? nl / dL : tl;
+                    tm = bad ? nm / dM : tm;
+                    ts = bad ? ns / dS : ts;
                 }
-                p0 = g; p1 = g; p2 = g;
-                n = 1;
+                const auto t = xyz(tl, tm, ts);
+                const float tMin = fminf(t.c[0], fminf(t.c[1], t.c[2])) + kEps;
+                nj = t.c[0] == tMin ? 0u : (t.c[1] == tMin ? 1u : 2u);
+                oL = oL + tMin * dL; oM = oM + tMin * dM; oS = oS + tMin * dS;
+                gL = f2i(floorf(oL)); gM = f2i(floorf(oM)); gS = f2i(floorf(oS));
+                if (!grid_in_region(gL, gM, gS)) { exitk = 2u; break; }   // left the region: no tail
+                CL = gL; CM = gM; CS = gS;
+                AM = gM; AS = gS;
             }
-            // ---- the mask words of all probe slots, requested together
-            const bool inr = (((uint32_t)p0.x | (uint32_t)p0.y | (uint32_t)p0.z | (uint32_t)p1.x | (uint32_t)p1.y |
-                               (uint32_t)p1.z) < 64u);   // p2 is in the region (tested above / = p0)
-            const uint32_t w0 = this->word_index((uint32_t)p0.x & 63u, (uint32_t)p0.y & 63u, (uint32_t)p0.z & 63u);
-            const uint32_t w1 = this->word_index((uint32_t)p1.x & 63u, (uint32_t)p1.y & 63u, (uint32_t)p1.z & 63u);
-            const uint32_t w2 = this->word_index((uint32_t)p2.x & 63u, (uint32_t)p2.y & 63u, (uint32_t)p2.z & 63u);
-            Blk b0 = mload(w0), b1 = mload(w1);
-            const Blk b2 = mload(w2);
+            // ---- the mask words of all slots, requested together
+            const uint32_t wA = word(gL, AM, AS), wB = word(gL, CM, CS), wC = word(CL, CM, CS);
+            const Blk bA = mload(wA), bB = mload(wB), bC = mload(wC);
+            // ---- evaluate the slots in the reference's order (A, B, C)
+            const uint32_t iA = bit5(gL, AM, AS), iB = bit5(gL, CM, CS), iC = bit5(CL, CM, CS);
+            const bool fA = (bA.x >> iA) & 1u, fB = (bB.x >> iB) & 1u, fC = (bC.x >> iC) & 1u;
+            const bool eA = vA && (absent(bA) || fA), eB = vB && (absent(bB) || fB);
+            stop = eA ? 0u : (eB ? 1u : ((absent(bC) || fC) ? 2u : 3u));
+            bool hit = eA ? fA : (eB ? fB : fC);
+            // the value index of the stopping slot only
+            const uint32_t sx = eA ? bA.x : (eB ? bB.x : bC.x), sy = eA ? bA.y : (eB ? bB.y : bC.y);
+            const uint32_t si = eA ? iA : (eB ? iB : iC);
+            col = sy + __popc(sx & ((1u << si) - 1u));
+            // huge grid coordinates (A or B outside the region; C is inside): the
+            // general (aliasing) form, rare
+            const bool inr = !vA || ((((uint32_t)gL | (uint32_t)AM | (uint32_t)AS) < 64u) &&
+                                     (!vB || (((uint32_t)gL | (uint32_t)CM | (uint32_t)CS) < 64u)));
+            if (COUNT && inr) {
+                const i3 P[3] = {to_i3(gL, AM, AS), to_i3(gL, CM, CS), to_i3(CL, CM, CS)};
+                const Blk B[3] = {bA, bB, bC};
+                const uint32_t W[3] = {wA, wB, wC};
+                const bool V[3] = {vA, vB, true};
+#pragma unroll
+                for (uint32_t i = 0; i < 3u; ++i) {
+                    if (!V[i] || i > stop) continue;
+                    this->count(4);                   // doesVoxelSpaceExist
+                    if (absent(B[i])) continue;
+                    const uint32_t bit = this->in_cluster(P[i].x, P[i].y, P[i].z) & 31u;
+                    this->count_bsearch(s.vcs_mask + (size_t)reg * 8192u + (W[i] & ~15u),
+                                        B[i].y + __popc(B[i].x & ((1u << bit) - 1u)), (B[i].x >> bit) & 1u);
+                }
+            }
             if (__builtin_expect(__builtin_amdgcn_ballot_w64(!inr) != 0, 0)) {
-                if (!inr) {       // huge grid coordinates: the general (aliasing) form
-                    b0 = this->mask_word(reg, p0.x, p0.y, p0.z);
-                    b1 = this->mask_word(reg, p1.x, p1.y, p1.z);
-                }
-            }
-            // ---- evaluate the slots in the reference's order
-            uint32_t stop = n, col = kEmpty;
-            bool hit = false;
-            auto eval = [&](uint32_t i, const i3& p, const Blk& b, uint32_t wi) {
-                if (i >= n || stop != n) return;
-                this->count(4);                       // doesVoxelSpaceExist
-                if (absent(b)) { stop = i; return; }
-                uint32_t c;
-                if (((uint32_t)p.x | (uint32_t)p.y | (uint32_t)p.z) < 64u) {
-                    const uint32_t bit = this->word_bit5((uint32_t)p.y, (uint32_t)p.z) & 31u;
-                    const bool found = (b.x >> bit) & 1u;
-                    const uint32_t vi = b.y + __popc(b.x & ((1u << bit) - 1u));
-                    if (COUNT) this->count_bsearch(mreg + (wi & ~15u), vi, found);
-                    c = found ? vi : kEmpty;          // value index (read below)
-                    if (found) { hit = true; stop = i; col = c; }
-                } else {
-                    c = this->lookup_aliased(reg, p.x, p.y, p.z);
-                    if (c != kEmpty) { hit = true; stop = i; col = c | 0x80000000u; }   // a colour, not an index
-                }
-            };
-            eval(0u, p0, b0, w0);
-            eval(1u, p1, b1, w1);
-            eval(2u, p2, b2, w2);
-            if (hit) {
-                const uint32_t v = (col & 0x80000000u) ? (col & 0x7FFFFFFFu) : s.vcs_vals[col];
-                if (!SHADOW) {
-                    h.col = v;
-                    h.region = cr;
-                    h.longest = true;
-                    if (jumping) {                   // performVoxelSpaceJump's hit
-                        h.n = normal_from_t(tX, tY, tZ, tMin, ds);
-                        h.so = old_o;
-                    } else {                         // an axis step's hit
-                        const uint32_t axis = stop == 0u ? a0 : (stop == 1u ? a1 : L);
-                        f3 nn = mk(0.0f, 0.0f, 0.0f);
-                        setf(nn, axis, copysignf(1.0f, -comp(ds, axis)));
-                        h.n = nn;
-                        if (axis == L) {
-                            h.so = ray_o;
-                        } else {                     // getLocalHitLocation (Renderer.cuh:753-758)
-                            const float o = comp(old_o, axis), dd = comp(ds, axis);
-                            const float t = dd > 0.0f ? (ceilf(o) - o) / dd : (floorf(o) - o) / dd;
-                            h.so = add(old_o, scl(t, ds));
+                if (!inr) {
+                    stop = 3u; hit = false; col = kEmpty;
+                    const i3 P[3] = {to_i3(gL, AM, AS), to_i3(gL, CM, CS), to_i3(CL, CM, CS)};
+                    const bool V[3] = {vA, vB, true};
+#pragma unroll
+                    for (uint32_t i = 0; i < 3u; ++i) {
+                        if (!V[i] || stop != 3u) continue;
+                        this->count(4);               // doesVoxelSpaceExist
+                        const Blk b = i == 2u ? bC : this->mask_word(reg, P[i].x, P[i].y, P[i].z);
+                        if (absent(b)) { stop = i; continue; }
+                        if (((uint32_t)P[i].x | (uint32_t)P[i].y | (uint32_t)P[i].z) < 64u) {
+                            const uint32_t bit = this->in_cluster(P[i].x, P[i].y, P[i].z) & 31u;
+                            const bool f = (b.x >> bit) & 1u;
+                            const uint32_t vi = b.y + __popc(b.x & ((1u << bit) - 1u));
+                            if (COUNT) this->count_bsearch(this->masks(reg, this->cluster_id(P[i].x, P[i].y, P[i].z)), vi, f);
+                            if (f) { stop = i; hit = true; col = vi; }
+                        } else {
+                            const uint32_t c = this->lookup_aliased(reg, P[i].x, P[i].y, P[i].z);
+                            if (c != kEmpty) { stop = i; hit = true; col = c | 0x80000000u; }
                         }
                     }
                 }
-                return true;
             }
-            if (jumping) {
-                if (stop == 0u) continue;            // still no cluster: skip again
+            if (hit) { exitk = 1u; break; }
+            if (jumping && stop == 3u) {
                 // landed in an existing cluster without a hit: CONTINUE_VAL (:740-750)
-                const float oL = comp(old_o, L);
-                const float tNext = dsL > 0.0f ? (ceilf(oL) - oL) / dsL : (floorf(oL) - oL) / dsL;
-                ray_o = add(old_o, scl(tNext + kEps, ds));
-                seti(ad, M, f2i(comp(ray_o, M)) - geti(g, M));
-                seti(ad, S, f2i(comp(ray_o, S)) - geti(g, S));
-                jumping = false;
-                continue;
+                const float nn = (dL > 0.0f ? ceilf(oL) : floorf(oL)) - oL;
+                float tNext = div_fast(nn, qL);
+                const bool bad = !(qL.ok && (nn == 0.0f || fabsf(nn) >= 0x1p-90f));
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) tNext = bad ? nn / dL : tNext;
+                rL = oL + (tNext + kEps) * dL; rM = oM + (tNext + kEps) * dM; rS = oS + (tNext + kEps) * dS;
             }
-            if (stop != n) {                         // an absent cluster: performVoxelSpaceJump
-                g = stop == 0u ? p0 : (stop == 1u ? p1 : p2);
-                this->count(4);                      // its first existence test (this same cell)
-                jumping = true;
-                continue;
+            if (!jumping) {
+                if (stop != 3u) {                    // an absent cluster: performVoxelSpaceJump
+                    this->count(4);                  // its first existence test (this same cell)
+                } else {                             // end of the iteration (:903-906)
+                    oL = rL; oM = rM; oS = rS;
+                    rL = rL + dL; rM = rM + dM; rS = rS + dS;
+                }
+                // g = the stopping slot (A, B or C), C at the end of the iteration
+                gL = stop == 3u || stop == 2u ? CL : gL;
+                gM = stop == 0u ? AM : CM;
+                gS = stop == 0u ? AS : CS;
             }
-            g = p2;                                  // end of the iteration (:903-906)
-            old_o = ray_o;
-            ray_o = add(ray_o, ds);
-            seti(ad, M, f2i(comp(ray_o, M)) - geti(g, M));
-            seti(ad, S, f2i(comp(ray_o, S)) - geti(g, S));
+            aM = f2i(rM) - gM;                       // (recomputed from unchanged values: same)
+            aS = f2i(rS) - gS;
+            jumping = stop != 3u;                    // jump on / start a jump; CONTINUE_VAL ends one
         }
-        oo = old_o;     // Renderer.cuh:912 (direction of originalRay kept)
-        return grid_original<SHADOW>(oo, od, reg, cr, h);
+        if (exitk == 1u) {
+            // the hit as {colour, normal code, location in oo} from the loop's final
+            // state: the caller makes the Hit after the original-DDA tail
+            if (!SHADOW) {
+                hcol = (col & 0x80000000u) ? (col & 0x7FFFFFFFu) : s.vcs_vals[col];
+                // normal: axis a (x, y, z) with copysignf(1, -ds[a]): code = a | sign(ds[a]) << 2
+                auto code = [](uint32_t a, float d) { return a | ((__float_as_uint(d) >> 31) << 2); };
+                if (jumping) {                       // performVoxelSpaceJump's hit (getNormalFromTValues)
+                    const auto d = xyz(dL, dM, dS);
+                    hcode = code(nj, nj == 0u ? d.c[0] : (nj == 1u ? d.c[1] : d.c[2]));
+                    oo = to_f3(oL, oM, oS);
+                } else if (stop == 2u) {             // the L step's hit
+                    hcode = code(PL, dL);
+                    oo = to_f3(rL, rM, rS);
+                } else {                             // a crossing's hit: getLocalHitLocation (:753-758)
+                    const bool onM = (stop == 0u) == mfirst;
+                    const float o = onM ? oM : oS, dd = onM ? dM : dS;
+                    hcode = onM ? code(PM, dM) : code(PS, dS);
+                    const float t = dd > 0.0f ? (ceilf(o) - o) / dd : (floorf(o) - o) / dd;
+                    oo = to_f3(oL + t * dL, oM + t * dM, oS + t * dS);
+                }
+            }
+            return true;
+        }
+        oo = to_f3(oL, oM, oS);     // Renderer.cuh:912 (direction of originalRay kept)
+        tail = exitk == 0u;
+        return false;
+    }
+    template <bool SHADOW>
+    __device__ __forceinline__ bool grid_longest_vcs(f3& oo, f3 od, uint32_t reg, i3 cr, Hit& h) {
+        // the axis order of convertRayToLongestAxisDirection (Ray.cuh:19-71)
+        const float ax = fabsf(od.x), ay = fabsf(od.y), az = fabsf(od.z);
+        const uint32_t order = (ax > ay && ax > az) ? (ay > az ? 0u : 1u) : (ay > az ? (ax > az ? 2u : 3u) : (ax > ay ? 4u : 5u));
+        bool hit = false, tail = false, todo = true;
+        uint32_t hcol = 0, hcode = 0;
+        while (todo) {                                // one pass per order present in the wave
+            const uint32_t pat = __builtin_amdgcn_readfirstlane(order);
+            if (order == pat) {
+                todo = false;
+                switch (pat) {
+                    case 0: hit = walk_longest_vcs<SHADOW, 0, 1, 2>(oo, od, reg, tail, hcol, hcode); break;
+                    case 1: hit = walk_longest_vcs<SHADOW, 0, 2, 1>(oo, od, reg, tail, hcol, hcode); break;
+                    case 2: hit = walk_longest_vcs<SHADOW, 1, 0, 2>(oo, od, reg, tail, hcol, hcode); break;
+                    case 3: hit = walk_longest_vcs<SHADOW, 1, 2, 0>(oo, od, reg, tail, hcol, hcode); break;
+                    case 4: hit = walk_longest_vcs<SHADOW, 2, 0, 1>(oo, od, reg, tail, hcol, hcode); break;
+                    default: hit = walk_longest_vcs<SHADOW, 2, 1, 0>(oo, od, reg, tail, hcol, hcode); break;
+                }
+            }
+        }
+        if (aborted) return false;
+        if (tail) return grid_original<SHADOW>(oo, od, reg, cr, h);
+        if (!SHADOW && hit) {
+            const float one = (hcode & 4u) ? 1.0f : -1.0f;
+            const uint32_t a = hcode & 3u;
+            h.col = hcol;
+            h.n = mk(a == 0u ? one : 0.0f, a == 1u ? one : 0.0f, a == 2u ? one : 0.0f);
+            h.so = oo;
+            h.region = cr;
+            h.longest = true;
+        }
+        return hit;
     }
 
     // rayMarchVoxelScene (Renderer.cuh:338-434) / rayMarchVoxelSceneLongestAxis (:917-1010).
