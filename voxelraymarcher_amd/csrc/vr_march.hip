@@ -152,6 +152,9 @@ __device__ __forceinline__ bool crawl_voxel(float on, float c, int32_t& q) {
 // CUs more tightly (per frame in flight: C2 0.151 -> 0.1415 ms, C3 0.420 -> 0.385,
 // C4 0.101 -> 0.096; one tile per workgroup: C2 0.1423, C3 0.377, C4 0.0955).
 constexpr uint32_t kTilesX = 2, kTilesY = 1;
+#ifndef VR_LONG_TAIL_GENERIC
+#define VR_LONG_TAIL_GENERIC false
+#endif
 
 // CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
 // crawling ray reserves an entry in the launch's deferral list and unwinds.
@@ -195,9 +198,11 @@ struct Walker : Ctx<STORE, COUNT> {
     // rs (crawl pass only): a deferral record -- resume the walk at its crawl.
     // rc: the ray's reciprocals rcp_setup(d.x), (d.y), (d.z), made once per ray
     // (nullptr: made here).
+    // generic: one loop for every sign pattern (the longest-axis walks' rare
+    // original-DDA tails: less code and register demand in that kernel)
     __device__ __forceinline__ bool grid_original_rt(f3& o, f3 d, uint32_t reg, i3 cr, Hit& h, const bool SHADOW,
                                                      const bool EQ, const uint32_t* rs = nullptr,
-                                                     const Rcp* rc = nullptr) {
+                                                     const Rcp* rc = nullptr, const bool generic = false) {
         const bool resume = CRAWL && rs != nullptr;
         VR_DIAG_COUNT(SHADOW ? 9 : 8);                 // grid_original calls
         const bool px = d.x > 0.0f, py = d.y > 0.0f, pz = d.z > 0.0f;
@@ -385,7 +390,7 @@ struct Walker : Ctx<STORE, COUNT> {
                     const uint32_t sg = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
                     using N = Sgn<-1>;
                     using P = Sgn<1>;
-                    if (CRAWL) {
+                    if (CRAWL || generic) {
                         walk(Sgn<0>{}, Sgn<0>{}, Sgn<0>{});
                     } else {
                         // One pass of the loop specialised for each sign pattern present in
@@ -780,18 +785,21 @@ struct Walker : Ctx<STORE, COUNT> {
         }
         int32_t aM = f2i(rM) - gM, aS = f2i(rS) - gS;
         const bool mid_floor = dM < 0.0f;                                 // decimalToIntFunc (:784)
-        // the walk's reciprocals: its divisions by dL, dM, dS are div_fast (IEEE
-        // fallback off the domain)
-        const Rcp qL = rcp_setup(dL), qM = rcp_setup(dM), qS = rcp_setup(dS);
-        const bool qok = qL.ok && qM.ok && qS.ok;
+        // (IEEE divisions: hoisted reciprocals (div_fast) measured slower here, C3
+        // 0.385 -> 0.413 ms -- three more VGPRs live through the loop)
         const uint32_t moff = reg << 16;              // SGPR-base loads (see grid_original_rt)
         auto mload = [&](uint32_t w) {
             return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) + (moff | (w << 3)));
         };
         uint32_t nj = 0;                  // the jump's last skip: getNormalFromTValues' axis (x, y, z)
         bool jumping = false;
-        uint32_t exitk = 0, stop = 3u, col = 0;   // loop exit: 0 = tail, 1 = hit, 2 = left the region
+        uint32_t stop = 3u, col = 0;
         bool mfirst = false;
+        // One exit per iteration (each extra exit of a divergent loop costs lane-mask
+        // bookkeeping on every iteration): a lane that must leave computes the rest
+        // of the iteration on stale values and leaves at its end, with the reason
+        enum : uint32_t { kGo = 0, kHit = 1, kLeft = 2, kBudget = 3, kTail = 4 };
+        uint32_t why = kGo, it = this->iters;
         VR_DIAG_COUNT(SHADOW ? 19 : 17);               // longest-axis walks
         for (;;) {
             VR_DIAG_COUNT(SHADOW ? 20 : 18);           // longest-axis loop iterations
@@ -800,18 +808,17 @@ struct Walker : Ctx<STORE, COUNT> {
             int32_t AM, AS, CL, CM, CS;
             bool vA = false, vB = false;
             mfirst = false;
+            uint32_t ex;
             if (!jumping) {
                 CL = gL + aL; CM = gM + aM; CS = gS + aS;
-                if (!grid_in_region(CL, CM, CS)) break;   // exitk 0: the original-DDA tail
-                if (!tick()) return false;
+                // the loop condition (else the original-DDA tail), then tick()
+                const bool out = !grid_in_region(CL, CM, CS);
+                it += out ? 0u : 1u;
+                ex = out ? kTail : (it > kIterBudget ? kBudget : kGo);
                 const bool hasM = aM != 0, hasS = aS != 0;
                 bool sfirst = false;
                 if (hasM && hasS) {
-                    // (the numerator is +0 or in (-1, 1): div_fast's domain is |n| >= 2^-90)
-                    const float n1 = (mid_floor ? floorf(oM) : ceilf(oM)) - oM;
-                    float t1 = div_fast(n1, qM);
-                    const bool bad = !(qM.ok && (n1 == 0.0f || fabsf(n1) >= 0x1p-90f));
-                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) t1 = bad ? n1 / dM : t1;
+                    const float t1 = ((mid_floor ? floorf(oM) : ceilf(oM)) - oM) / dM;
                     const float sp = oS + dS * t1;
                     sfirst = f2i(floorf(sp)) - gS != 0;
                 }
@@ -821,28 +828,18 @@ struct Walker : Ctx<STORE, COUNT> {
                 AM = mfirst ? CM : gM;
                 AS = mfirst ? gS : CS;
             } else {
-                if (!tick()) return false;
+                ++it;                                // tick()
+                ex = it > kIterBudget ? kBudget : kGo;
                 // performVoxelSpaceJump's cluster skip (:707-725), integer planes from g
                 const int32_t nL = dL > 0.0f ? ((gL / 8) + 1) * 8 : (gL / 8) * 8;
                 const int32_t nM = dM > 0.0f ? ((gM / 8) + 1) * 8 : (gM / 8) * 8;
                 const int32_t nS = dS > 0.0f ? ((gS / 8) + 1) * 8 : (gS / 8) * 8;
-                const float nl = (float)nL - oL, nm = (float)nM - oM, ns = (float)nS - oS;
-                float tl = div_fast(nl, qL), tm = div_fast(nm, qM), ts = div_fast(ns, qS);
-                // (numerators of in-region cells are < 73; +0 divides exactly but takes the
-                // IEEE branch here, rarely)
-                const bool bad = !(qok && fminf(fabsf(nl), fminf(fabsf(nm), fabsf(ns))) >= 0x1p-90f &&
-                                   fmaxf(fabsf(nl), fmaxf(fabsf(nm), fabsf(ns))) <= 0x1p+20f);
-                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                    tl = bad ? nl / dL : tl;
-                    tm = bad ? nm / dM : tm;
-                    ts = bad ? ns / dS : ts;
-                }
-                const auto t = xyz(tl, tm, ts);
+                const auto t = xyz(((float)nL - oL) / dL, ((float)nM - oM) / dM, ((float)nS - oS) / dS);
                 const float tMin = fminf(t.c[0], fminf(t.c[1], t.c[2])) + kEps;
                 nj = t.c[0] == tMin ? 0u : (t.c[1] == tMin ? 1u : 2u);
                 oL = oL + tMin * dL; oM = oM + tMin * dM; oS = oS + tMin * dS;
                 gL = f2i(floorf(oL)); gM = f2i(floorf(oM)); gS = f2i(floorf(oS));
-                if (!grid_in_region(gL, gM, gS)) { exitk = 2u; break; }   // left the region: no tail
+                if (ex == kGo && !grid_in_region(gL, gM, gS)) ex = kLeft;   // left the region: no tail
                 CL = gL; CM = gM; CS = gS;
                 AM = gM; AS = gS;
             }
@@ -861,9 +858,9 @@ struct Walker : Ctx<STORE, COUNT> {
             col = sy + __popc(sx & ((1u << si) - 1u));
             // huge grid coordinates (A or B outside the region; C is inside): the
             // general (aliasing) form, rare
-            const bool inr = !vA || ((((uint32_t)gL | (uint32_t)AM | (uint32_t)AS) < 64u) &&
-                                     (!vB || (((uint32_t)gL | (uint32_t)CM | (uint32_t)CS) < 64u)));
-            if (COUNT && inr) {
+            const bool inr = ex != kGo || !vA || ((((uint32_t)gL | (uint32_t)AM | (uint32_t)AS) < 64u) &&
+                                                  (!vB || (((uint32_t)gL | (uint32_t)CM | (uint32_t)CS) < 64u)));
+            if (COUNT && inr && ex == kGo) {
                 const i3 P[3] = {to_i3(gL, AM, AS), to_i3(gL, CM, CS), to_i3(CL, CM, CS)};
                 const Blk B[3] = {bA, bB, bC};
                 const uint32_t W[3] = {wA, wB, wC};
@@ -902,13 +899,13 @@ struct Walker : Ctx<STORE, COUNT> {
                     }
                 }
             }
-            if (hit) { exitk = 1u; break; }
+            if (ex != kGo || hit) {
+                why = ex != kGo ? ex : kHit;
+                break;
+            }
             if (jumping && stop == 3u) {
                 // landed in an existing cluster without a hit: CONTINUE_VAL (:740-750)
-                const float nn = (dL > 0.0f ? ceilf(oL) : floorf(oL)) - oL;
-                float tNext = div_fast(nn, qL);
-                const bool bad = !(qL.ok && (nn == 0.0f || fabsf(nn) >= 0x1p-90f));
-                if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) tNext = bad ? nn / dL : tNext;
+                const float tNext = ((dL > 0.0f ? ceilf(oL) : floorf(oL)) - oL) / dL;
                 rL = oL + (tNext + kEps) * dL; rM = oM + (tNext + kEps) * dM; rS = oS + (tNext + kEps) * dS;
             }
             if (!jumping) {
@@ -927,7 +924,12 @@ struct Walker : Ctx<STORE, COUNT> {
             aS = f2i(rS) - gS;
             jumping = stop != 3u;                    // jump on / start a jump; CONTINUE_VAL ends one
         }
-        if (exitk == 1u) {
+        this->iters = it;
+        if (why == kBudget) {
+            aborted = true;
+            return false;
+        }
+        if (why == kHit) {
             // the hit as {colour, normal code, location in oo} from the loop's final
             // state: the caller makes the Hit after the original-DDA tail
             if (!SHADOW) {
@@ -952,7 +954,7 @@ struct Walker : Ctx<STORE, COUNT> {
             return true;
         }
         oo = to_f3(oL, oM, oS);     // Renderer.cuh:912 (direction of originalRay kept)
-        tail = exitk == 0u;
+        tail = why == kTail;
         return false;
     }
     template <bool SHADOW>
@@ -977,7 +979,7 @@ struct Walker : Ctx<STORE, COUNT> {
             }
         }
         if (aborted) return false;
-        if (tail) return grid_original<SHADOW>(oo, od, reg, cr, h);
+        if (tail) return grid_original_rt(oo, od, reg, cr, h, SHADOW, false, nullptr, nullptr, VR_LONG_TAIL_GENERIC);
         if (!SHADOW && hit) {
             const float one = (hcode & 4u) ? 1.0f : -1.0f;
             const uint32_t a = hcode & 3u;
