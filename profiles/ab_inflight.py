@@ -19,6 +19,6 @@ for rnd in range(rounds):
         env = dict(os.environ, VR_LIBRARY=os.path.abspath(lib))
         r = subprocess.run([sys.executable, os.path.join(here, "inflight_probe.py"), cfg, K], env=env,
                            capture_output=True, text=True, timeout=600)
-        lines = [l for l in r.stdout.splitlines() if "streams=1" in l or "streams=2" in l] or [r.stderr[-400:]]
+        lines = [l for l in r.stdout.splitlines() if "streams=1" in l or "streams=2" in l or "digest" in l] or [r.stderr[-400:]]
         for l in lines:
             print(f"[{rnd}] {os.path.basename(lib)}: {l}", flush=True)

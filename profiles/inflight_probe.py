@@ -27,6 +27,8 @@ info = vr.VoxelSceneInfo((0, 0, 0), cfg.scale)
 ref = torch.empty(W * H, dtype=torch.int32, device="cuda")
 vr.run_raymarching_kernel(scene, cfg.algorithm, cam, lit, info, W, H, ref)
 torch.cuda.synchronize()
+_w = torch.arange(1, W * H + 1, dtype=torch.int64, device="cuda")
+print(f"{name} frame digest {int((ref.to(torch.int64) * _w).sum())} {int(ref.to(torch.int64).sum())}", flush=True)
 for S in (1, 2, 3, 4):
     streams = [torch.cuda.Stream() for _ in range(S)]
     outs = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in range(S)]

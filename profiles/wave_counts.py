@@ -24,7 +24,9 @@ NAMES = {0: "primary VCS walks (sign-specialised)", 1: "primary VCS walks (gener
          13: "shadow null-region skips", 14: "primary() calls", 15: "entry-clip iterations",
          16: "shadow walks started", 17: "primary longest-axis walks", 18: "primary longest-axis iterations",
          19: "shadow longest-axis walks", 20: "shadow longest-axis iterations",
-         21: "longest-axis iterations with a jumping lane"}
+         21: "longest-axis iterations with a jumping lane",
+         22: "primary iterations, no lane skipping", 23: "primary iterations, every lane skipping",
+         24: "shadow iterations, no lane skipping", 25: "shadow iterations, every lane skipping"}
 
 name = sys.argv[1] if len(sys.argv) > 1 else "C2"
 cfg = vr.CONFIGS[name]

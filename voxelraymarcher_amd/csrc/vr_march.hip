@@ -152,6 +152,15 @@ __device__ __forceinline__ bool crawl_voxel(float on, float c, int32_t& q) {
 // CUs more tightly (per frame in flight: C2 0.151 -> 0.1415 ms, C3 0.420 -> 0.385,
 // C4 0.101 -> 0.096; one tile per workgroup: C2 0.1423, C3 0.377, C4 0.0955).
 constexpr uint32_t kTilesX = 2, kTilesY = 1;
+// VR_UNIFORM_SKIP: the cluster-skip planes and their selects are computed only in
+// wave-iterations where some lane stands in an absent cluster (one uniform branch on
+// the ballot).  In C2, 61 % of the primary and 60 % of the shadow wave-iterations
+// have no skipping lane (VR_DIAG counters 22-25, profiles/r02/wave_counts_C2_skip.txt):
+// those run 51 VALU instead of 61.  C2 0.1172 -> 0.1113 ms per frame in flight,
+// identical pixels; C5 (sparse: mostly skips) 0.688 -> 0.697 (profiles/r02/ab_uniform_skip_*.txt).
+#ifndef VR_UNIFORM_SKIP
+#define VR_UNIFORM_SKIP 1
+#endif
 #ifndef VR_LONG_TAIL_GENERIC
 #define VR_LONG_TAIL_GENERIC false
 #endif
@@ -327,20 +336,41 @@ struct Walker : Ctx<STORE, COUNT> {
                             // both candidate planes, computed while the mask word is in
                             // flight and materialised (with the whole 8-B word: one load)
                             float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey), vZ = plane_v<SZ>(o.z, gz, ez);
+#if VR_UNIFORM_SKIP
+                            asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(blk.x), "+v"(blk.y));
+                            const bool skip = absent(blk);
+                            float nX = vX, nY = vY, nZ = vZ;
+                            if (__builtin_amdgcn_ballot_w64(skip) != 0) {
+                                float cX = (float)((vx & 0x38) + plane_c8<SX>(cx8)), cY = (float)((vy & 0x38) + plane_c8<SY>(cy8)),
+                                      cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
+                                nX = skip ? cX : vX; nY = skip ? cY : vY; nZ = skip ? cZ : vZ;
+                                asm volatile("" : "+v"(nX), "+v"(nY), "+v"(nZ));
+                            }
+#else
                             // (in the region v < 64, so v & ~7 == v & 0x38, the form word_index shares)
                             float cX = (float)((vx & 0x38) + plane_c8<SX>(cx8)), cY = (float)((vy & 0x38) + plane_c8<SY>(cy8)),
                                   cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
                             asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
                             const bool skip = absent(blk);
+#endif
+#ifdef VR_DIAG
+                            {   // wave-iterations where no active lane / every active lane skips a cluster
+                                const uint64_t bs = __builtin_amdgcn_ballot_w64(skip);
+                                if (bs == 0) VR_DIAG_COUNT(SHADOW ? 24 : 22);
+                                else if (bs == __builtin_amdgcn_read_exec()) VR_DIAG_COUNT(SHADOW ? 25 : 23);
+                            }
+#endif
                             bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
                             // 0 or ~0 (an absent cluster's words have no bits set)
                             const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)blk.x, bit, 1u);
                             found = fm != 0u;
                             vi = blk.y + __popc(blk.x & ((1u << (bit & 31u)) - 1u));
                             if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
+#if !VR_UNIFORM_SKIP
                             const float nX = skip ? cX : vX;
                             const float nY = skip ? cY : vY;
                             const float nZ = skip ? cZ : vZ;
+#endif
                             const float ax = nX - o.x, ay = nY - o.y, az = nZ - o.z;
                             float sMin;
                             crawl = false;
