@@ -158,6 +158,8 @@ constexpr uint32_t kTilesX = 2, kTilesY = 1;
 // have no skipping lane (VR_DIAG counters 22-25, profiles/r02/wave_counts_C2_skip.txt):
 // those run 51 VALU instead of 61.  C2 0.1172 -> 0.1113 ms per frame in flight,
 // identical pixels; C5 (sparse: mostly skips) 0.688 -> 0.697 (profiles/r02/ab_uniform_skip_*.txt).
+// A three-way form (voxel planes only when some lane does not skip, so they wait for the
+// load) measured slower: C2 0.1112 -> 0.1147, C5 0.688 -> 0.694 (ab_uniform_skip3_*.txt).
 #ifndef VR_UNIFORM_SKIP
 #define VR_UNIFORM_SKIP 1
 #endif
@@ -335,8 +337,8 @@ struct Walker : Ctx<STORE, COUNT> {
                             __builtin_amdgcn_sched_barrier(0);   // issue the load before the planes
                             // both candidate planes, computed while the mask word is in
                             // flight and materialised (with the whole 8-B word: one load)
-                            float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey), vZ = plane_v<SZ>(o.z, gz, ez);
 #if VR_UNIFORM_SKIP
+                            float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey), vZ = plane_v<SZ>(o.z, gz, ez);
                             asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(blk.x), "+v"(blk.y));
                             const bool skip = absent(blk);
                             float nX = vX, nY = vY, nZ = vZ;
@@ -347,6 +349,7 @@ struct Walker : Ctx<STORE, COUNT> {
                                 asm volatile("" : "+v"(nX), "+v"(nY), "+v"(nZ));
                             }
 #else
+                            float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey), vZ = plane_v<SZ>(o.z, gz, ez);
                             // (in the region v < 64, so v & ~7 == v & 0x38, the form word_index shares)
                             float cX = (float)((vx & 0x38) + plane_c8<SX>(cx8)), cY = (float)((vy & 0x38) + plane_c8<SY>(cy8)),
                                   cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
