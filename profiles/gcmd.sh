@@ -1,9 +1,12 @@
-# one GPU call's steps: parity suite, round profile (rocprofv3 trace + PMC passes), bench lines
 set -o pipefail
-O=gpurun_out/h4
+O=gpurun_out/h9
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 &&
-bash profiles/run_round.sh r02b C2 > $O/run_round.txt 2>&1 &&
-cp gpurun_out/r02b/traffic.json profiles/traffic.json &&
-timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err &&
-timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench20.json 2>&1
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.txt 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/sched -o bench -- python3 bench.py --no-cpu-baseline --steps 50 > $O/log.txt 2>&1 &&
+for r in 1 2; do
+timeout -k 10 200 python bench.py --no-cpu-baseline > $O/bench_sched_$r.json 2>&1 &&
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-schedule > $O/bench_plain_$r.json 2>&1 || exit 1
+done &&
+timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 --warmup 5 > $O/bench_sched_20.json 2>&1 &&
+timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 --warmup 5 --no-schedule > $O/bench_plain_20.json 2>&1
