@@ -1,5 +1,7 @@
+# final check of the tree as committed: parity suite, smoke, driver-style bench
 set -o pipefail
-O=gpurun_out/h15
+O=gpurun_out/h16
 mkdir -p $O
-A=voxelraymarcher_amd/ab
-timeout -k 10 600 python profiles/ab_inflight.py C3 100 $A/libvr_lw6.so $A/libvr_lw5.so $A/libvr_lw4.so --rounds 2 > $O/ab_C3.txt 2>&1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 &&
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 &&
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench20.json 2>&1
