@@ -1,7 +1,5 @@
-# final check of the tree as committed: parity suite, smoke, driver-style bench
 set -o pipefail
-O=gpurun_out/h16
+O=gpurun_out/h17
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 &&
-timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 &&
-timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench20.json 2>&1
+A=voxelraymarcher_amd/ab
+timeout -k 10 600 python profiles/ab_inflight.py C2 400 $A/libvr_t21.so $A/libvr_t12.so $A/libvr_t41.so --rounds 2 > $O/ab_C2.txt 2>&1

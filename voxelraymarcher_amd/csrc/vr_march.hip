@@ -151,7 +151,13 @@ __device__ __forceinline__ bool crawl_voxel(float on, float c, int32_t& q) {
 // workgroup's slot is held until its slowest wave ends, so smaller ones pack the
 // CUs more tightly (per frame in flight: C2 0.151 -> 0.1415 ms, C3 0.420 -> 0.385,
 // C4 0.101 -> 0.096; one tile per workgroup: C2 0.1423, C3 0.377, C4 0.0955).
-constexpr uint32_t kTilesX = 2, kTilesY = 1;
+#ifndef VR_TILES_X
+#define VR_TILES_X 2
+#endif
+#ifndef VR_TILES_Y
+#define VR_TILES_Y 1
+#endif
+constexpr uint32_t kTilesX = VR_TILES_X, kTilesY = VR_TILES_Y;
 // VR_UNIFORM_SKIP: the cluster-skip planes and their selects are computed only in
 // wave-iterations where some lane stands in an absent cluster (one uniform branch on
 // the ballot).  In C2, 61 % of the primary and 60 % of the shadow wave-iterations
