@@ -1,37 +1,43 @@
 #!/usr/bin/env python3
-"""Benchmark: Mrays/s of the MI355X ray march on BASELINE.json's headline
-config (C2: 256^3 synthetic grid, VCS + original, 1920x1080), plus the
+"""Benchmark: Mrays/s of the MI355X ray march on a BASELINE.json config (default
+C2, the headline: 256^3 synthetic grid, VCS + original, 1920x1080), plus the
 roofline of the dominant kernel and the CPU oracle baseline.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
+                  [--tiling auto|weak|fixed]
 
-A step = one full frame.  N = 1: the C2 frame exactly.  N > 1 (one rank per
-GPU, torch.distributed.run, RCCL): weak scaling over image tiles -- the same
-view at N x the pixels (each side x sqrt(N), ~1920x1080 per GPU), rows split
-into interleaved 8-row bands (band b -> rank b % N), and every frame gathered
-to rank 0 over RCCL as RGB8 (3 B per pixel) and assembled there.  Two frames are in flight
-(tiles.BandGather: two band buffers, each with its own stream): the long waves
-that end frame k overlap the start of frame k+1, and frame k's gather runs beside
-frame k+1's render.  Every frame is still rendered in full.  Inputs (scene,
-camera) are resident in HBM before timing starts; the timed region ends after
-the last frame's gather and assembly.  Rank 0 prints ONE JSON line.
+A step = one full frame.  The frame's rows are cut into interleaved 8-row bands
+(band b -> rank b % N); each rank renders its bands and every frame is gathered to
+rank 0 over RCCL as RGB8 (3 B per pixel) and assembled there.  Tiling:
+  fixed -- the config's own frame whatever N is (strong scaling; BASELINE C5 is
+           defined this way: one 3840x2160 frame tiled over 8 GPUs);
+  weak  -- the same view at about N x the pixels (each side x sqrt(N));
+  auto  -- fixed for C5, weak for the others (default).
+Two frames are in flight (tiles.BandGather: two band buffers, each with its own
+stream): the long waves that end frame k overlap the start of frame k+1, and frame
+k's gather runs beside frame k+1's render.  Every frame is still rendered in full.
+Inputs (scene, camera) are resident in HBM before timing starts; the timed region
+ends after the last frame's gather and assembly.  Rank 0 prints ONE JSON line.
 
 `value`/`ms_per_step` are the pipelined throughput; `kernel_ms` is one launch
 timed alone (HIP events on the launch stream, nothing overlapping).
-roofline.achieved = the algorithmic bytes of one launch / that
-launch's average duration `kernel_ms` (the figure rocprofv3's per-dispatch
-duration reproduces); `achieved_pipelined` = the same bytes x launches per second
-in the timed loop (two launches overlap there).  The scene is
-L2/MALL-resident, so those bytes are mostly served on-die: the roofline also
-carries the PMC-measured HBM bytes (traffic, hbm_measured_*) and the VALU-issue
-fraction that actually bounds the walk (valu_issue_frac), both from the
-round's profile (profiles/traffic.json, written by profiles/collect_traffic.py).
+
+roofline: `achieved`/`frac` are the north star's figure -- the algorithmic bytes
+of one launch (the words the reference walk reads, counted by the
+instrumented kernel) / that launch's average duration `kernel_ms` / 8 TB/s.
+`bound` is the MEASURED limiter, from the round's PMC profile
+(profiles/traffic.json, keyed by config, written by profiles/collect_traffic.py):
+"valu" when the walk's VALU issue is closer to its roof than the measured HBM
+traffic is to the HBM roof (every VCS config: the scene is L2/MALL-resident),
+else "hbm".  The line carries both fractions: `hbm_measured_frac` (PMC DRAM
+bytes) and `valu_issue_frac` (VALU issue cycles / the chip's SIMD cycles).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -43,10 +49,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import voxelraymarcher_amd as vr  # noqa: E402
-from voxelraymarcher_amd.tiles import BandGather, weak_scaled_resolution  # noqa: E402
+from voxelraymarcher_amd.tiles import BandGather, frame_resolution  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+N_SIMD = 1024              # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles (SIMD-32)
 BAND_ROWS = 8              # one wave tile high
+HEADLINE = "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s"   # BASELINE.json metric
 
 
 def parse():
@@ -55,45 +63,116 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="C2", choices=sorted(vr.CONFIGS))
+    p.add_argument("--tiling", default="auto", choices=["auto", "weak", "fixed"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--frames-in-flight", type=int, default=2,
                    help="band buffers/streams of the frame pipeline (1 = one frame at a time, for PMC passes)")
-    p.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (default min(16, cpus))")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="oracle threads (default: the CPUs this process may run on, at most OMP_NUM_THREADS)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                   help="PMC-derived HBM bytes per launch (written by profiles/collect_traffic.py)")
+                   help="PMC-derived HBM bytes and VALU issue per launch, keyed by config "
+                        "(written by profiles/collect_traffic.py)")
     return p.parse_args()
 
 
+def cpu_info() -> dict:
+    """The host CPU as lscpu names it, and how many logical CPUs the machine has."""
+    info = {"machine_cpus": os.cpu_count()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() == "Model name":
+                info["model"] = v.strip()
+            elif k.strip() == "Socket(s)":
+                info["sockets"] = int(v.strip())
+            elif k.strip() == "Core(s) per socket":
+                info["cores_per_socket"] = int(v.strip())
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    return info
+
+
+def baseline_threads() -> int:
+    """All the CPUs this process may use (its affinity mask), capped by
+    OMP_NUM_THREADS when set: on a shared GPU box the affinity mask / OMP limit is
+    the box's CPU share (16 per GPU), while os.cpu_count() reports the whole machine."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def _oracle_rate(scene, cam, lit, cfg, threads: int, cpu_seconds: float):
-    """Whole frames of the config, repeated until about `cpu_seconds` of CPU
-    time (threads x wall) has been spent, after one untimed frame."""
+    """Rays per second of the oracle on a bounded sample of the config's frame: evenly
+    spaced 8-row bands (every `stride`-th band; the whole frame when that fits the
+    budget), repeated until about `cpu_seconds` of CPU time (threads x wall) has been
+    spent, after one untimed pass."""
+    W, H = cfg.width, cfg.height
+    bands = list(range(0, H, 8))
+
+    def run(sel):
+        for y in sel:
+            scene.render(int(cfg.algorithm), cam, lit, W, H, cfg.scale, row_begin=y, row_end=min(H, y + 8),
+                         nthreads=threads)
+        return sum(min(H, y + 8) - y for y in sel) * W
+
+    # probe 1/64 of the bands to size the sample
     t0 = time.perf_counter()
-    scene.render(int(cfg.algorithm), cam, lit, cfg.width, cfg.height, cfg.scale, nthreads=threads)
-    first = time.perf_counter() - t0
-    reps = int(min(60, max(1, np.ceil(cpu_seconds / max(first * threads, 1e-3)))))
+    rays = run(bands[::64])
+    per_ray = (time.perf_counter() - t0) * threads / rays
+    stride = max(1, int(np.ceil(per_ray * W * H / cpu_seconds)))
+    sel = bands[::stride]
+    run(sel)                                                           # untimed
+    one = max(per_ray * len(sel) * 8 * W, 1e-3)
+    reps = int(min(60, max(1, np.floor(cpu_seconds / one))))
     t0 = time.perf_counter()
+    rays = 0
     for _ in range(reps):
-        scene.render(int(cfg.algorithm), cam, lit, cfg.width, cfg.height, cfg.scale, nthreads=threads)
+        rays += run(sel)
     dt = time.perf_counter() - t0
-    return reps, dt, cfg.width * cfg.height * reps / dt / 1e6
+    return rays, dt, rays / dt / 1e6, stride
 
 
 def cpu_baseline(cfg, xyz, rgb, threads: int) -> dict:
-    """Oracle (clean-room C restatement, OpenMP dynamic over 8x8 tiles) on the
-    host cores over the same workload: on `threads` cores (~16
-    CPU-s) and on one core (~4 s)."""
+    """The oracle (clean-room C restatement, -O3, OpenMP dynamic over rows) on the host
+    cores over the same workload: on `threads` cores (~20 CPU-s) and on
+    one core (~6 s)."""
     import oracle
     scene = oracle.Scene(xyz, rgb, int(cfg.store))
     cam = oracle.reference_camera(cfg.width, cfg.height)
     lit = oracle.lighting()
-    reps, dt, rate = _oracle_rate(scene, cam, lit, cfg, threads, 16.0)
-    reps1, dt1, rate1 = _oracle_rate(scene, cam, lit, cfg, 1, 4.0)
-    rays = cfg.width * cfg.height * reps
+    rays, dt, rate, stride = _oracle_rate(scene, cam, lit, cfg, threads, 20.0)
+    rays1, dt1, rate1, stride1 = _oracle_rate(scene, cam, lit, cfg, 1, 6.0)
+    ci = cpu_info()
+
+    def sample(r, s, t, n):
+        part = "the whole frame" if s == 1 else f"every {s}th 8-row band of the frame"
+        return (f"{r} primary rays of {cfg.name} ({part}, repeated) in {t:.2f} s wall on {n} thread(s) "
+                f"({t * n:.1f} CPU-s), oracle/vr_oracle.c -O3 OpenMP")
+
     return {"value": round(rate, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} full {cfg.width}x{cfg.height} frames of {cfg.name} ({rays} primary rays, "
-                      f"{dt * threads:.1f} CPU-s), oracle/vr_oracle.c -O2 OpenMP {threads} threads, {dt:.2f} s wall",
+            "sample": sample(rays, stride, dt, threads),
+            "cpu_model": ci.get("model"), "machine_cpus": ci.get("machine_cpus"),
+            "threads_note": "all CPUs of this process's affinity mask, capped by OMP_NUM_THREADS (the GPU "
+                            "box's CPU share); machine_cpus is the whole host",
             "single_core": {"value": round(rate1, 3), "unit": "Mrays/s", "cores": 1,
-                            "sample": f"{reps1} full frames, {dt1:.2f} s"}}
+                            "sample": sample(rays1, stride1, dt1, 1)}}
+
+
+def load_traffic(path: str, cfg_name: str, world: int) -> dict:
+    """The round's PMC profile of this config (profiles/traffic.json): {config: {...}},
+    or the round-2 single-config form."""
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    if "config" in tj:                                   # round-2 form: one config
+        tj = {tj["config"]: tj}
+    t = tj.get(cfg_name, {})
+    return t if t.get("world", 1) == world else {}
 
 
 def main():
@@ -110,9 +189,10 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     cfg = vr.CONFIGS[args.config]
+    tiling = args.tiling if args.tiling != "auto" else ("fixed" if cfg.name == "C5" else "weak")
     xyz, rgb = cfg.voxels()
     scene = vr.create_scene(xyz, rgb, cfg.store, device=local)
-    W, H = weak_scaled_resolution(cfg.width, cfg.height, world)
+    W, H = frame_resolution(cfg.width, cfg.height, world, tiling)
     cam = vr.Camera.reference(W, H)
     lit = vr.setup_constant_values()
     info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
@@ -140,11 +220,11 @@ def main():
     pipe.drain()
     torch.cuda.synchronize()
 
-    # kernel-only timing of this rank's launch on the launch stream (HIP events),
-    # at least 200 launches (~35 ms of C2 work): enough samples for kernel_ms, and
-    # the GPU reaches its loaded clock before the timed loop starts (a short
-    # --steps run otherwise measures the clock ramp of a GPU that sat idle while
-    # the host built the scene)
+    # kernel-only timing of this rank's launch on the launch stream (HIP events; the
+    # events bracket the whole launch: tile pass + crawl pass), at least 200 launches:
+    # enough samples for kernel_ms, and the GPU reaches its loaded clock before the
+    # timed loop starts (a short --steps run otherwise measures the clock ramp of a
+    # GPU that sat idle while the host built the scene)
     n_iso = max(args.steps, 200)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_iso)]
     for a, b in ev:
@@ -192,44 +272,53 @@ def main():
     mrays = W * H / (ms_per_step * 1e-3) / 1e6
 
     if rank == 0:
-        achieved = launch_bytes / (ms_per_step * 1e-3) / 1e9          # launches overlap: pipelined rate
         achieved_isolated = launch_bytes / (kern_ms * 1e-3) / 1e9
-        traffic, tj = None, {}
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("config") == cfg.name and tj.get("world") == world:
-                traffic = tj.get("hbm_bytes_per_launch")
-            else:
-                tj = {}
-        except (OSError, ValueError):
-            pass
-        roof = {"bound": "hbm", "achieved": round(achieved_isolated, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        achieved_pipe = launch_bytes / (ms_per_step * 1e-3) / 1e9    # this GPU's launches overlap in the loop
+        tj = load_traffic(args.traffic_json, cfg.name, world)
+        traffic = tj.get("hbm_bytes_per_launch")
+        roof = {"bound": None, "achieved": round(achieved_isolated, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved_isolated / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "achieved_basis": "algorithmic bytes per launch (SURVEY 8(d): the words the reference walk reads, "
                                   "counted by the instrumented kernel) / the launch's average duration (kernel_ms, "
-                                  "HIP events on the launch stream)",
-                "achieved_pipelined": round(achieved, 1),
-                "frac_pipelined": round(achieved / HBM_PEAK_GBS, 4),
+                                  "HIP events on the launch stream) -- the north star's figure, mostly served "
+                                  "from L2/MALL, not HBM",
+                "achieved_pipelined": round(achieved_pipe, 1),
+                "frac_pipelined": round(achieved_pipe / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": launch_bytes, "algorithmic_bytes_per_frame": frame_bytes}
+        hbm_frac = valu_frac = None
         if traffic:
-            # what HBM actually serves: the scene is L2/MALL-resident, so the measured
-            # DRAM bytes (PMC, profiles/) are a small fraction of the algorithmic ones
-            hbm = traffic / (kern_ms * 1e-3) / 1e9                      # per launch, as achieved
-            roof.update({"hbm_measured_gbs": round(hbm, 1), "hbm_measured_frac": round(hbm / HBM_PEAK_GBS, 4),
+            # what HBM actually serves (PMC DRAM bytes per launch, profiles/)
+            hbm = traffic / (kern_ms * 1e-3) / 1e9
+            hbm_frac = hbm / HBM_PEAK_GBS
+            roof.update({"hbm_measured_gbs": round(hbm, 1), "hbm_measured_frac": round(hbm_frac, 4),
                          "algorithmic_over_hbm_bytes": round(launch_bytes / traffic, 1)})
         if tj.get("valu_insts_per_launch") and tj.get("grbm_gui_active_per_launch") and tj.get("rocprof_avg_ns"):
-            # the limiter: VALU issue of the dependent walk (2 cycles per wave64
-            # instruction on each of the 1024 SIMD-32s) at the clock the profile measured
-            cyc = tj["grbm_gui_active_per_launch"] / 8.0                 # GRBM sums the 8 XCDs
+            # VALU issue of the dependent walk: 2 cycles per wave64 instruction on each of the
+            # 1024 SIMD-32s, at the clock the profile measured (GRBM_GUI_ACTIVE sums the 8 XCDs)
+            cyc = tj["grbm_gui_active_per_launch"] / 8.0
             ghz = cyc / tj["rocprof_avg_ns"]
             valu_cyc = 2.0 * tj["valu_insts_per_launch"]
-            roof["limiter"] = "VALU issue and memory latency of the per-pixel walk (not HBM bandwidth)"
-            roof["valu_issue_frac"] = round(valu_cyc / (1024 * ghz * ms_per_step * 1e6), 4)
-            roof["valu_issue_frac_isolated"] = round(valu_cyc / (1024 * cyc), 4)
+            valu_frac = valu_cyc / (N_SIMD * cyc)
+            roof["valu_issue_frac"] = round(valu_frac, 4)                       # one launch alone
+            roof["valu_issue_frac_pipelined"] = round(valu_cyc / (N_SIMD * ghz * ms_per_step * 1e6), 4)
+            roof["valu_insts_per_launch"] = tj["valu_insts_per_launch"]
             roof["profile_clock_ghz"] = round(ghz, 3)
+            if tj.get("lane_util") is not None:
+                roof["valu_lane_utilisation"] = tj["lane_util"]
+        if hbm_frac is not None and valu_frac is not None:
+            roof["bound"] = "valu" if valu_frac >= hbm_frac else "hbm"
+            roof["bound_basis"] = ("the measured limiter: VALU issue fraction vs measured HBM fraction "
+                                   f"({valu_frac:.3f} vs {hbm_frac:.3f}, profiles/traffic.json)")
+        else:
+            roof["bound"] = "valu" if cfg.store == vr.StorageType.VOXEL_CLUSTER_STORE else "hbm"
+            roof["bound_basis"] = "no PMC profile of this config in profiles/traffic.json: by store"
+        metric = HEADLINE if cfg.name == "C2" else \
+            (f"Mrays/sec at {cfg.width}x{cfg.height}, {cfg.grid}^3 grid ({cfg.store.name}+{cfg.algorithm.name}); "
+             f"achieved HBM GB/s")
+        par = f"row-band tiles x{world}" + (" + RCCL gather of the RGB8 bands to rank 0 (overlapped with the "
+                                             "next frame)" if world > 1 else "")
         line = {
-            "metric": "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s",
+            "metric": metric,
             "value": round(mrays, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -237,18 +326,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if tiling == "fixed" else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (counter-hash voxel grid, SURVEY.md 8(d))",
-            "config": {"workload": f"{cfg.name}: {cfg.notes}" + (
-                           "" if world == 1 else f"; the same view at {W}x{H} (x{world} pixels, weak scaling)"),
-                       "grid": cfg.grid, "width": W, "height": H,
+            "config": {"workload": f"{cfg.name}: {cfg.notes}, {W}x{H}" + (
+                           "" if world == 1 or tiling == "fixed" else f" (the same view at x{world} pixels, weak "
+                                                                       f"scaling)"),
+                       "grid": cfg.grid, "width": W, "height": H, "tiling": tiling,
                        "store": cfg.store.name, "algorithm": cfg.algorithm.name, "scale": cfg.scale,
-                       "voxels": int(len(rgb)), "parallelism": f"row-band tiles x{world}" +
-                       (" + RCCL gather of the RGB8 bands to rank 0 (overlapped with the next frame)"
-                        if world > 1 else ""),
-                       "frames_in_flight": pipe.depth},
+                       "voxels": int(len(rgb)), "parallelism": par, "frames_in_flight": pipe.depth},
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_median": round(kern_median, 4),
             "kernel_mrays_per_s": round(W * H / world / (kern_ms * 1e-3) / 1e6, 2),
@@ -257,8 +344,7 @@ def main():
         if frame_latency_ms is not None:
             line["frame_latency_ms"] = round(frame_latency_ms, 4)
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(cfg, xyz, rgb, threads)
+            line["cpu_baseline"] = cpu_baseline(cfg, xyz, rgb, args.cpu_threads or baseline_threads())
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -151,12 +151,12 @@ int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
 /* Number of uint32 words vr_render_bands writes per rank. */
 uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t nranks);
 
-/* Kernel implementations behind vr_render*: all produce identical pixels. */
+/* Kernel implementations behind vr_render*: all produce identical pixels.
+ * (Value 2 was a persistent state-machine kernel, retired in round 3: it was
+ * never the fastest; it is rejected with VR_E_INVALID.) */
 typedef enum {
     VR_KERNEL_AUTO = 0,         /* the fastest measured for the (store, algorithm) pair */
     VR_KERNEL_TILE = 1,         /* one lane per pixel, one wave per 8x8 tile (vr_march.hip) */
-    VR_KERNEL_PERSISTENT = 2,   /* persistent state machine: one voxel probe per lane-iteration,
-                                   primary + shadow rays fused, tile queue (vr_persist.hip) */
     VR_KERNEL_TILE_REWALK = 3   /* the tile kernel whose crawl pass walks every deferred pixel
                                    from its start instead of resuming it (cross-check) */
 } vr_kernel;
@@ -172,6 +172,8 @@ typedef struct {
     uint32_t band_rows;   /* 0 = one band covering [row_begin,row_end) */
     uint32_t rank, nranks;
     uint64_t* bytes_dev;
+    uint32_t defer_cap;   /* records in the crawl pass's deferral list: 0 = the default (16384);
+                             smaller values exercise its overflow path (tests) */
 } vr_render_opts;
 int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
                  const float translation[3], uint32_t scale, uint32_t width, uint32_t height,

@@ -80,8 +80,18 @@ def lib() -> ctypes.CDLL:
         L.or_pixel_stats.argtypes = [c_void_p, c_int, POINTER(OrCamera), POINTER(OrLighting), POINTER(c_float),
                                      c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, POINTER(c_uint64), c_int]
         L.or_pixel_stats.restype = c_int
+        L.or_set_iter_budget.argtypes = [c_uint64]
+        L.or_set_iter_budget.restype = None
         _lib = L
     return _lib
+
+
+NO_BUDGET = (1 << 64) - 1
+
+
+def set_iter_budget(budget: int = NO_BUDGET) -> None:
+    """Diagnostic iteration budget of every later render (process-global; see vr_oracle.h)."""
+    lib().or_set_iter_budget(int(budget))
 
 
 def _f3(v):
@@ -166,10 +176,11 @@ class Scene:
 
     def pixel_stats(self, algo: int, cam: OrCamera, lit: OrLighting, width: int, height: int, scale: int,
                     translation=(0.0, 0.0, 0.0), row_begin: int = 0, row_end: int | None = None, nthreads: int = 0):
-        """-> uint64[rows, width, 2, 7]: per-pixel (primary, shadow) x (region reads, existence
-        checks, cluster skips, lookups, probes, hits, iterations)."""
+        """-> uint64[rows, width, 2, 9]: per-pixel (primary, shadow) x (region reads, existence
+        checks, cluster skips, lookups, probes, hits, iterations, existence checks outside the
+        region, aliased ones among them)."""
         row_end = height if row_end is None else row_end
-        st = np.zeros(((row_end - row_begin), width, 2, 7), dtype=np.uint64)
+        st = np.zeros(((row_end - row_begin), width, 2, 9), dtype=np.uint64)
         rc = lib().or_pixel_stats(self.h, int(algo), ctypes.byref(cam), ctypes.byref(lit), _f3(translation),
                                   int(scale), int(width), int(height), int(row_begin), int(row_end),
                                   st.ctypes.data_as(POINTER(c_uint64)), int(nthreads))

@@ -12,12 +12,15 @@
  * what the CUDA device code does), and float->int conversions use the CUDA
  * device semantics (truncate, saturate, NaN -> 0).
  *
- * One deliberate, documented deviation (DESIGN.md "Hang guard"): every
- * pixel has an iteration budget of VR_ITER_BUDGET loop iterations over all
- * its loops (primary + shadow).  The reference would spin forever on the
- * degenerate rays that exhaust it (e.g. NaN origins, or ulp-sized steps);
- * here the pixel becomes background (0).  The HIP kernel implements the
- * identical budget, so parity is unaffected.
+ * No iteration budget: every walk runs to the end the reference reaches,
+ * however many iterations that takes (C5's cluster-skip crawls run up to
+ * ~1.4 million).  The one deliberate, documented deviation is
+ * for walks the reference never finishes: a loop iteration that leaves the
+ * loop's whole state bit-for-bit unchanged repeats forever (every loop below
+ * is a deterministic function of that state), so the pixel is declared
+ * non-terminating there -- colour 0 and only the pixel write counted (4 B).
+ * Those are the `stationary` checks below; they are exact (a state that does
+ * not change cannot reach an exit), they never fire on a walk that ends.
  */
 #include "vr_oracle.h"
 
@@ -34,7 +37,10 @@
 #define CONTINUE_VAL (EMPTY_VAL + 2u)  /* VoxelFunctions.cuh:23 */
 #define BLOCK 64                       /* VoxelFunctions.cuh:24 */
 #define CLUSTER 8                      /* VoxelFunctions.cuh:25 */
-#define VR_ITER_BUDGET 65536u
+
+/* Iteration budget per pixel (or_set_iter_budget; UINT64_MAX = none, the
+ * default): a diagnostic only -- the restatement runs without one. */
+static uint64_t g_budget = UINT64_MAX;
 
 /* ------------------------------------------------------------------ math */
 
@@ -80,6 +86,8 @@ static inline uint32_t f2u(float f) {
     if (f >= 4294967296.0f) return UINT32_MAX;
     return (uint32_t)f;
 }
+
+void or_set_iter_budget(uint64_t budget) { g_budget = budget; }
 
 /* ------------------------------------------------------------ the scene */
 
@@ -323,7 +331,7 @@ typedef struct {
     const or_lighting* lit;
     v3f translation;
     uint64_t bytes;
-    uint32_t iters;
+    uint64_t iters;
     int aborted;
     int in_shadow;          /* statistics only: counting into st[1] while walking a shadow ray */
     uint64_t* st;           /* optional work statistics, OR_STAT_* x 2 (primary, shadow) */
@@ -331,15 +339,27 @@ typedef struct {
 
 /* work statistics (or_render_stats) */
 enum { OR_STAT_REGION = 0, OR_STAT_EXISTS, OR_STAT_SKIP, OR_STAT_LOOKUP, OR_STAT_PROBE, OR_STAT_HIT,
-       OR_STAT_ITERS, OR_STAT_N };
+       OR_STAT_ITERS, OR_STAT_OUTSIDE, OR_STAT_ALIAS, OR_STAT_N };
 #define STAT(c, k) do { if ((c)->st) (c)->st[(c)->in_shadow * OR_STAT_N + (k)]++; } while (0)
 
 static inline int tick(ctx* c) {
     if (c->aborted) return 0;
     STAT(c, OR_STAT_ITERS);
-    if (++c->iters > VR_ITER_BUDGET) { c->aborted = 1; return 0; }
+    if (++c->iters > g_budget) { c->aborted = 1; return 0; }
     return 1;
 }
+
+/* Loop state comparison for the non-termination checks: the same bits, or both
+ * NaN (NaN payloads may change once; every later use treats them alike). */
+static inline int same_f(float a, float b) {
+    uint32_t x, y;
+    memcpy(&x, &a, 4); memcpy(&y, &b, 4);
+    return x == y || (a != a && b != b);
+}
+static inline int same_v(v3f a, v3f b) { return same_f(a.v[0], b.v[0]) && same_f(a.v[1], b.v[1]) && same_f(a.v[2], b.v[2]); }
+static inline int same_i(v3i a, v3i b) { return a.v[0] == b.v[0] && a.v[1] == b.v[1] && a.v[2] == b.v[2]; }
+/* The loop would repeat this iteration forever: give up on the pixel. */
+static inline int stationary(ctx* c) { c->aborted = 1; return 0; }
 
 /* VoxelScene::isRayInScene (Renderer.cuh:38-44) */
 static inline int in_scene(const ctx* c, v3i r) {
@@ -364,6 +384,10 @@ static inline int space_exists(ctx* c, int32_t reg, int32_t x, int32_t y, int32_
     c->bytes += 4;
     STAT(c, OR_STAT_EXISTS);
     int32_t cid = cluster_id_short(x, y, z);
+    if (((uint32_t)x | (uint32_t)y | (uint32_t)z) >= (uint32_t)BLOCK) {
+        STAT(c, OR_STAT_OUTSIDE);                         /* a probe outside the region */
+        if (cid >= 0 && cid < 512) STAT(c, OR_STAT_ALIAS); /* ... whose short id aliases a cluster */
+    }
     if (cid < 0 || cid >= 512) { STAT(c, OR_STAT_SKIP); return 0; }
     if (c->s->vcs_dir[(size_t)reg * 512 + (size_t)cid] >= 0) return 1;
     STAT(c, OR_STAT_SKIP);
@@ -539,6 +563,7 @@ static uint32_t shadow_grid_original(ctx* c, ray3* ray, int32_t reg) {
             float sZ = d.v[2] != 0.0f ? ((float)cz - o.v[2]) / d.v[2] : INFINITY;
             float sMin = fminf(sX, fminf(sY, sZ));
             ray->o = vadd(o, vscale(sMin + EPS, d));
+            if (same_v(ray->o, o)) return stationary(c), EMPTY_VAL;
             continue;
         }
         uint32_t col = lookup_voxel(c, reg, vx, vy, vz);
@@ -549,6 +574,7 @@ static uint32_t shadow_grid_original(ctx* c, ray3* ray, int32_t reg) {
         tZ = d.v[2] != 0.0f ? (nZ - o.v[2]) / d.v[2] : INFINITY;
         tMin = fminf(tX, fminf(tY, tZ));
         ray->o = vadd(o, vscale(tMin + EPS, d));
+        if (same_v(ray->o, o)) return stationary(c), EMPTY_VAL;
     }
     return EMPTY_VAL;
 }
@@ -559,15 +585,19 @@ static int shadow_scene_original(ctx* c, ray3 lr, v3i cr) {
     c->in_shadow = 1;
     while (in_scene(c, cr)) {
         if (!tick(c)) return 0;
+        const v3i cr0 = cr; const v3f o0 = lr.o;
         int32_t reg = region_at(c, cr);
         while (reg < 0) {
             if (!tick(c)) return 0;
+            const v3i cr1 = cr; const v3f o1 = lr.o;
             if (!skip_null_region(c, &cr, &lr, 1, &reg)) return 0;
+            if (same_i(cr, cr1) && same_v(lr.o, o1)) return stationary(c);
         }
         uint32_t col = shadow_grid_original(c, &lr, reg);
         if (c->aborted) return 0;
         if (col != EMPTY_VAL) return 1;
         advance_region(&cr, &lr);
+        if (same_i(cr, cr0) && same_v(lr.o, o0)) return stationary(c);
     }
     return 0;
 }
@@ -598,6 +628,7 @@ static uint32_t grid_original(ctx* c, ray3* ray, v3f rwp, int32_t reg, v3i cr) {
             float sZ = ((float)cz - o.v[2]) / d.v[2];
             float sMin = fminf(sX, fminf(sY, sZ));
             ray->o = vadd(o, vscale(sMin + EPS, d));
+            if (same_v(ray->o, o)) return stationary(c), EMPTY_VAL;
             continue;
         }
         uint32_t col = lookup_voxel(c, reg, vx, vy, vz);
@@ -613,6 +644,7 @@ static uint32_t grid_original(ctx* c, ray3* ray, v3f rwp, int32_t reg, v3i cr) {
         tZ = (nZ - o.v[2]) / d.v[2];
         tMin = fminf(tX, fminf(tY, tZ));
         ray->o = vadd(o, vscale(tMin + EPS, d));
+        if (same_v(ray->o, o)) return stationary(c), EMPTY_VAL;
     }
     return EMPTY_VAL;
 }
@@ -653,6 +685,7 @@ static uint32_t voxel_space_jump(ctx* c, ray3* orig, v3f rwp, int32_t reg, ray3*
     while (!space_exists(c, reg, g[0], g[1], g[2])) {
         if (!tick(c)) return EMPTY_VAL;
         v3f o = old->o, d = old->d;
+        v3i g0 = {{g[0], g[1], g[2]}};
         int32_t nx = d.v[0] > 0.0f ? ((g[0] / 8) + 1) * 8 : (g[0] / 8) * 8;
         int32_t ny = d.v[1] > 0.0f ? ((g[1] / 8) + 1) * 8 : (g[1] / 8) * 8;
         int32_t nz = d.v[2] > 0.0f ? ((g[2] / 8) + 1) * 8 : (g[2] / 8) * 8;
@@ -668,6 +701,8 @@ static uint32_t voxel_space_jump(ctx* c, ray3* orig, v3f rwp, int32_t reg, ray3*
             orig->o = old->o;                 /* direction of originalRay kept */
             return EMPTY_VAL;
         }
+        v3i g1 = {{g[0], g[1], g[2]}};
+        if (same_v(old->o, o) && same_i(g1, g0)) return stationary(c), EMPTY_VAL;
     }
     uint32_t col = lookup_voxel(c, reg, g[0], g[1], g[2]);
     if (col != EMPTY_VAL) {
@@ -774,15 +809,19 @@ static int shadow_scene_longest(ctx* c, ray3 lr, v3i cr) {
     c->in_shadow = 1;
     while (in_scene(c, cr)) {
         if (!tick(c)) return 0;
+        const v3i cr0 = cr; const v3f o0 = lr.o;
         int32_t reg = region_at(c, cr);
         while (reg < 0) {
             if (!tick(c)) return 0;
+            const v3i cr1 = cr; const v3f o1 = lr.o;
             if (!skip_null_region(c, &cr, &lr, 0, &reg)) return 0;
+            if (same_i(cr, cr1) && same_v(lr.o, o1)) return stationary(c);
         }
         uint32_t col = grid_longest(c, &lr, V3(0, 0, 0), reg, cr, 1);
         if (c->aborted) return 0;
         if (col != EMPTY_VAL) return 1;
         advance_region(&cr, &lr);
+        if (same_i(cr, cr0) && same_v(lr.o, o0)) return stationary(c);
     }
     return 0;
 }
@@ -797,6 +836,7 @@ static uint32_t scene_march(ctx* c, ray3 world, uint32_t scale, int algo) {
     /* entry clip (:349-373) */
     while (!in_scene(c, cr)) {
         if (!tick(c)) return 0;
+        const v3i cr0 = cr; const v3f o0 = sr.o;
         int32_t hi = (int32_t)(s->D + (uint32_t)s->min_coord), lo = 0 + s->min_coord;
         int32_t nx = d.v[0] < 0.0f ? hi : lo, ny = d.v[1] < 0.0f ? hi : lo, nz = d.v[2] < 0.0f ? hi : lo;
         float tX = ((float)(nx * BLOCK) - sr.o.v[0]) / d.v[0];
@@ -811,15 +851,19 @@ static uint32_t scene_march(ctx* c, ray3 world, uint32_t scale, int algo) {
         cr.v[0] = f2i(floorf(sr.o.v[0] / (float)BLOCK));
         cr.v[1] = f2i(floorf(sr.o.v[1] / (float)BLOCK));
         cr.v[2] = f2i(floorf(sr.o.v[2] / (float)BLOCK));
+        if (same_i(cr, cr0) && same_v(sr.o, o0)) return stationary(c);
     }
     ray3 lr = {vscale(1.0f, vsub(sr.o, V3((float)(cr.v[0] * BLOCK), (float)(cr.v[1] * BLOCK),
                                           (float)(cr.v[2] * BLOCK)))), d};
     while (in_scene(c, cr)) {
         if (!tick(c)) return 0;
+        const v3i cr0 = cr; const v3f o0 = lr.o;
         int32_t reg = region_at(c, cr);
         while (reg < 0) {
             if (!tick(c)) return 0;
+            const v3i cr1 = cr; const v3f o1 = lr.o;
             if (!skip_null_region(c, &cr, &lr, 0, &reg)) return 0;
+            if (same_i(cr, cr1) && same_v(lr.o, o1)) return stationary(c);
         }
         v3f rwp = vadd(c->translation, V3((float)(cr.v[0] * BLOCK), (float)(cr.v[1] * BLOCK),
                                           (float)(cr.v[2] * BLOCK)));
@@ -828,6 +872,7 @@ static uint32_t scene_march(ctx* c, ray3 world, uint32_t scale, int algo) {
         if (c->aborted) return 0;
         if (col != EMPTY_VAL) return col;
         advance_region(&cr, &lr);
+        if (same_i(cr, cr0) && same_v(lr.o, o0)) return stationary(c);
     }
     return 0;
 }
@@ -879,7 +924,7 @@ static uint32_t render_pixel(const or_scene* s, int algo, const or_camera* cam, 
     ctx c; memset(&c, 0, sizeof c);
     c.s = s; c.lit = lit; c.translation = tr; c.st = st;
     uint32_t col = scene_march(&c, world, scale, algo);
-    if (c.aborted) col = 0;
+    if (c.aborted) { col = 0; c.bytes = 0; }   /* never finishes: only the write counts */
     c.bytes += 4;                /* the pixel write */
     if (bytes) *bytes = c.bytes;
     return col;
@@ -926,8 +971,10 @@ int or_render_pixels(const or_scene* s, int algo, const or_camera* cam, const or
 }
 
 /* Work statistics of rows [row_begin,row_end): st[2*OR_STAT_N] = counts of
- * region reads, existence checks, cluster skips, lookups, probes, hits and
- * loop iterations, for primary (st[0..6]) and shadow (st[7..13]) walks. */
+ * region reads, existence checks, cluster skips, lookups, probes, hits, loop
+ * iterations, existence checks outside the region and those of them whose
+ * `short` cluster id aliases into the directory, for primary (st[0..8]) and
+ * shadow (st[9..17]) walks. */
 int or_render_stats(const or_scene* s, int algo, const or_camera* cam, const or_lighting* lit,
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
                     uint32_t row_begin, uint32_t row_end, uint64_t* st) {

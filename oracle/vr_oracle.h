@@ -73,6 +73,11 @@ uint32_t or_scene_region_count(const or_scene* s);
 uint32_t or_scene_lookup(const or_scene* s, int32_t rx, int32_t ry, int32_t rz,
                          int32_t x, int32_t y, int32_t z);
 
+/* Diagnostic: an iteration budget per pixel for every later render
+ * (process-global; UINT64_MAX = none, the default).  A pixel that exceeds it
+ * renders as 0 with 4 bytes, like a walk that never finishes. */
+void or_set_iter_budget(uint64_t budget);
+
 /* Known-answer helpers. */
 int32_t or_hash1(int32_t key, uint32_t offset);                 /* CuckooHashTable.cuh:181-190 */
 int32_t or_hash2(int32_t key, uint32_t prime);                  /* CuckooHashTable.cuh:193-202 */
@@ -95,13 +100,15 @@ int or_render_pixels(const or_scene* s, int algo, const or_camera* cam, const or
                      const uint32_t* px, const uint32_t* py, size_t n, uint32_t* out,
                      uint64_t* bytes_per_pixel);
 
-/* Work statistics (single-threaded): 2 x 7 counters, primary then shadow:
- * region reads, existence checks, cluster skips, lookups, key probes, hits, loop iterations. */
+/* Work statistics (single-threaded): 2 x 9 counters, primary then shadow:
+ * region reads, existence checks, cluster skips, lookups, key probes, hits, loop iterations,
+ * existence checks at coordinates outside [0,64), and those whose `short` cluster id still
+ * lands in the directory (VoxelClusterStore.cuh:21-24 aliasing). */
 int or_render_stats(const or_scene* s, int algo, const or_camera* cam, const or_lighting* lit,
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
                     uint32_t row_begin, uint32_t row_end, uint64_t* st);
 
-/* Per-pixel version: st[(r * width + x) * 14 + k] for row r - row_begin. OpenMP. */
+/* Per-pixel version: st[(r * width + x) * 18 + k] for row r - row_begin. OpenMP. */
 int or_pixel_stats(const or_scene* s, int algo, const or_camera* cam, const or_lighting* lit,
                    const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
                    uint32_t row_begin, uint32_t row_end, uint64_t* st, int nthreads);

@@ -6,14 +6,23 @@ Written separately from oracle/vr_oracle.c, from the reference source text
 transcription errors in the C oracle: the tests run both on the same rays and
 demand identical packed pixels.  Slow -- meant for a few hundred rays.
 
-Storage is a plain dict per region {local key: colour} plus the set of
-non-empty 8^3 clusters; lookups return the same values as VoxelClusterStore /
-CuckooHashTable (any correct structure does), and the VCS existence test is
-the cluster set (VoxelClusterStore.cuh:93-99).
+Storage is a sorted array of (region, local key) with the colours plus the
+sorted set of non-empty 8^3 clusters; lookups return the same values as
+VoxelClusterStore / CuckooHashTable (any correct structure does), and the VCS
+existence test is the cluster set (VoxelClusterStore.cuh:93-99).
+
+No iteration budget.  Walks that the reference never finishes (a loop
+iteration that leaves the loop's state unchanged repeats forever) render as
+0.  Cluster-skip crawls -- an axis pinned on its skip plane that EPSILON * d
+cannot move, so every iteration in the cluster moves the ray by RN(EPSILON *
+d) -- are run in closed form with exact rational arithmetic (crawl_run), a
+formulation independent of the GPU's float fast-forward (vr_march.hip
+crawl_steps) and of the C oracle, which walks them iteration by iteration.
 """
 from __future__ import annotations
 
 import math
+from fractions import Fraction
 
 import numpy as np
 
@@ -92,23 +101,128 @@ def fmin3(a, b, c):
     return np.fmin(a, np.fmin(b, c))
 
 
+def same(a, b) -> bool:
+    """Loop state equality for the never-finishes test: equal bits, or both NaN."""
+    for i in range(3):
+        x, y = F(a[i]), F(b[i])
+        if not (x.view(np.uint32) == y.view(np.uint32) or (x != x and y != y)):
+            return False
+    return True
+
+
+def _rne(q: Fraction) -> int:
+    """Round to nearest integer, ties to even."""
+    f = q.numerator // q.denominator
+    r = q - f
+    if r > Fraction(1, 2) or (r == Fraction(1, 2) and f % 2):
+        return f + 1
+    return f
+
+
+def crawl_run(p, d, lo):
+    """Closed form of a cluster-skip crawl.  p: the position a crawl iteration
+    (t = 0 on an axis pinned on its skip plane) produced; every further
+    iteration whose start lies in the same cluster [lo_i, lo_i + 8) is the same
+    skip, p_i <- RN(p_i + c_i) with c_i = RN(EPSILON * d_i).  Per axis, in units
+    of its ulp u: p_i = m u, and RN(m u + c_i) = (m + k) u with k =
+    rne(m + c_i / u) - m, constant while p_i stays in its binade (for a tie
+    c_i / u = j + 1/2 from the second step on: ties to even keep m even).
+    Returns (n, q): n >= 0 iterations whose start positions p, ..., q-step all
+    lie in the cluster and whose results q stays in it (n = 0: none), or
+    (None, p) when no coordinate moves at all (the crawl never ends)."""
+    n = None
+    ks = []
+    pinned = False
+    for i in range(3):
+        x = F(p[i])
+        c = F(EPS * F(d[i]))
+        if not (lo[i] <= float(x) < lo[i] + 8):
+            return 0, p
+        if F(x + c) == x:                        # the axis never moves
+            ks.append(None)
+            pinned |= float(d[i]) < 0 and float(x) == lo[i]
+            continue
+        if not float(x) >= 2.0 ** -100:
+            return 0, p
+        fr, e = math.frexp(float(x))             # x = fr 2^e, fr in [1/2, 1)
+        u = Fraction(2) ** (e - 24)
+        m = int(Fraction(float(x)) / u)          # 2^23 <= m < 2^24
+        q = Fraction(float(c)) / u
+        k0 = _rne(m + q) - m
+        k1 = _rne(m + k0 + q) - (m + k0)
+        if k0 != k1 or k0 == 0:                   # tie from an odd mantissa: step once more
+            return 0, p
+        if k0 > 0:
+            # every position m + t k (t <= n) below the binade's top and the cluster's
+            # upper plane (then every exact sum m + t k + q rounds at spacing u)
+            hi_int = min(2 ** 24, (lo[i] + 8) / u) - 1
+            na = int((hi_int - m) // k0)
+        else:
+            # positions at or above the cluster's lower plane, and every exact sum
+            # m + t k + q (t < n) at or above the binade's bottom: a sum below it
+            # rounds at the finer spacing of the binade beneath
+            na = int(min((m - Fraction(lo[i]) / u) // (-k0), (m + q - 2 ** 23) // (-k0) + 1))
+        n = na if n is None else min(n, na)
+        ks.append((m, k0, u))
+    if not pinned:
+        return 0, p
+    if n is None:
+        return None, p
+    if n <= 0:
+        return 0, p
+    out = []
+    for i in range(3):
+        if ks[i] is None:
+            out.append(F(p[i]))
+        else:
+            m, k, u = ks[i]
+            out.append(F(float((m + n * k) * u)))
+    return n, V(*out)
+
+
+
 class Scene:
     def __init__(self, xyz, rgb, store: int):
-        """VoxelSceneCPU::insertVoxel (VoxelSceneCPU.cuh:16-46) over the voxels."""
+        """VoxelSceneCPU::insertVoxel (VoxelSceneCPU.cuh:16-46) over the voxels: region =
+        floorf(x / 64.0f), local = ((x % 64) + 64) % 64, min/max region coordinate
+        scalars starting at 0, later duplicates win (map assignment, :46)."""
         self.store = store
-        self.regions = {}
-        mn = mx = 0
-        for (x, y, z), c in zip(np.asarray(xyz).tolist(), np.asarray(rgb).tolist()):
-            r = tuple(f2i(np.floor(F(v) / F(64))) for v in (x, y, z))
-            loc = tuple(((v % 64) + 64) % 64 for v in (x, y, z))   # Python % is already non-negative
-            mn = min(mn, *r)
-            mx = max(mx, *r)
-            key = (loc[0] << 20) | (loc[1] << 10) | loc[2]
-            self.regions.setdefault(r, {})[key] = int(c)
-        self.min = mn
-        self.D = mx - mn + 1
-        self.clusters = {r: {((k >> 20) // 8, ((k >> 10) & 0x3FF) // 8, (k & 0x3FF) // 8) for k in d}
-                         for r, d in self.regions.items()}
+        xyz = np.asarray(xyz, dtype=np.int64).reshape(-1, 3)
+        rgb = np.asarray(rgb, dtype=np.int64).reshape(-1)
+        r = np.floor(xyz.astype(np.float32) / np.float32(64)).astype(np.int64)
+        loc = np.mod(xyz, 64)
+        self.min = int(min(0, r.min())) if len(r) else 0
+        self.D = (int(max(0, r.max())) if len(r) else 0) - self.min + 1
+        rid = self._rid_np(r)
+        key = (loc[:, 0] << 20) | (loc[:, 1] << 10) | loc[:, 2]
+        comb = (rid << 32) | key
+        # the last insertion of a (region, key) wins: first occurrence in the reversed list
+        u, first = np.unique(comb[::-1], return_index=True)
+        self.keys = u
+        self.vals = rgb[::-1][first]
+        self.region_ids = np.unique(rid)
+        cl = (rid << 9) | ((loc[:, 0] // 8) << 6) | ((loc[:, 1] // 8) << 3) | (loc[:, 2] // 8)
+        self.clusters = np.unique(cl)
+
+    def _rid_np(self, r):
+        a = r - self.min
+        return a[:, 0] + a[:, 1] * self.D + a[:, 2] * self.D * self.D
+
+    def region_id(self, r):
+        a = [v - self.min for v in r]
+        rid = a[0] + a[1] * self.D + a[2] * self.D * self.D
+        i = np.searchsorted(self.region_ids, rid)
+        return rid if i < len(self.region_ids) and self.region_ids[i] == rid else None
+
+    def has_cluster(self, rid, cid):
+        c = (rid << 9) | cid
+        i = np.searchsorted(self.clusters, c)
+        return bool(i < len(self.clusters) and self.clusters[i] == c)
+
+    def get(self, rid, key):
+        c = (rid << 32) | key
+        i = np.searchsorted(self.keys, c)
+        return int(self.vals[i]) if i < len(self.keys) and self.keys[i] == c else EMPTY
 
 
 class Lighting:
@@ -134,17 +248,19 @@ class Walk:
         if self.aborted:
             return False
         self.iters += 1
-        if self.iters > 65536:
-            self.aborted = True
-            return False
         return True
+
+    def forever(self):
+        """The loop would repeat its last iteration forever: the pixel never finishes."""
+        self.aborted = True
+        return False
 
     # VoxelScene (Renderer.cuh:20-45)
     def in_scene(self, r):
         return all(u32(v - self.s.min) < self.s.D for v in r)
 
     def region(self, r):
-        return tuple(r) if tuple(r) in self.s.regions else None
+        return self.s.region_id(r)
 
     # StorageStructure adapters (StorageStructure.cuh:24-52)
     def exists(self, reg, x, y, z):
@@ -154,11 +270,11 @@ class Walk:
         cid = (((ux // 8) << 6) | ((uy // 8) << 3) | (uz // 8)) & 0xFFFF
         if cid >= 0x8000 or cid >= 512:            # `short` id outside the directory
             return False
-        return (cid >> 6, (cid >> 3) & 7, cid & 7) in self.s.clusters[reg]
+        return self.s.has_cluster(reg, cid)
 
     def lookup(self, reg, x, y, z):
         key = u32((u32(x) << 20) | (u32(y) << 10) | u32(z))
-        return self.s.regions[reg].get(key, EMPTY)
+        return self.s.get(reg, key)
 
     # lighting (Renderer.cuh:57-86, 249-258; VoxelFunctions.cuh:69-83)
     @staticmethod
@@ -236,7 +352,17 @@ class Walk:
                     q = int(vv / 8)      # C truncating division
                     nb.append((q + 1) * 8 if pos[i] else q * 8)
                 st = [self.div(F(nb[i]) - o[i], d[i], shadow) for i in range(3)]
-                ray[0] = o + d.scale(fmin3(*st) + EPS)
+                smin = fmin3(*st)
+                ray[0] = o + d.scale(smin + EPS)
+                if same(ray[0], o):
+                    self.forever()
+                    return EMPTY
+                if smin == 0:                    # a crawl: the identical iterations after it at once
+                    n, ray[0] = crawl_run(ray[0], d, [(v // 8) * 8 for v in (vx, vy, vz)])
+                    if n is None:
+                        self.forever()
+                        return EMPTY
+                    self.iters += n
                 continue
             col = self.lookup(reg, vx, vy, vz)
             if col != EMPTY:
@@ -247,6 +373,9 @@ class Walk:
             t = [self.div(self.nxt(pos[i], o[i]) - o[i], d[i], shadow) for i in range(3)]
             tMin = fmin3(*t)
             ray[0] = o + d.scale(tMin + EPS)
+            if same(ray[0], o):
+                self.forever()
+                return EMPTY
         return EMPTY
 
     def null_skip(self, lr, cr, guard):       # :386-409 / :187-210
@@ -262,13 +391,17 @@ class Walk:
         while self.in_scene(cr):
             if not self.tick():
                 return False
+            cr0, o0 = list(cr), lr[0]
             reg = self.region(cr)
             while reg is None:
                 if not self.tick():
                     return False
+                cr1, o1 = list(cr), lr[0]
                 self.null_skip(lr, cr, not longest)
                 if not self.in_scene(cr):
                     return False
+                if cr == cr1 and same(lr[0], o1):
+                    return self.forever()
                 reg = self.region(cr)
             col = self.grid_la(lr, reg, V(0, 0, 0), cr, True) if longest else self.grid(lr, reg, None, cr, True)
             if self.aborted:
@@ -276,6 +409,8 @@ class Walk:
             if col != EMPTY:
                 return True
             lr[0] = self.shift_region(cr, lr[0])
+            if cr == cr0 and same(lr[0], o0):
+                return self.forever()
         return False
 
     # rayMarchVoxelGridLongestAxis (:760-915) / shadow twin (:495-631)
@@ -322,13 +457,26 @@ class Walk:
                     q = int(g[i] / 8)
                     nb.append((q + 1) * 8 if ds[i] > 0 else q * 8)
                 tX, tY, tZ = (self.div(F(nb[i]) - o[i], ds[i]) for i in range(3))
-                tMin = fmin3(tX, tY, tZ) + EPS
+                tm0 = fmin3(tX, tY, tZ)
+                tMin = tm0 + EPS
                 st["old"] = o + ds.scale(tMin)
+                g0 = list(g)
                 for i in range(3):
                     g[i] = f2i(np.floor(st["old"][i]))
                 if not self.grid_in(*g):
                     orig[0] = st["old"].copy()
                     return EMPTY
+                if same(st["old"], o) and g == g0:
+                    self.forever()
+                    return EMPTY
+                if tm0 == 0:                     # a crawl (as in grid): closed form
+                    n, st["old"] = crawl_run(st["old"], ds, [(v // 8) * 8 for v in g0])
+                    if n is None:
+                        self.forever()
+                        return EMPTY
+                    self.iters += n
+                    for i in range(3):
+                        g[i] = f2i(np.floor(st["old"][i]))
             col = self.lookup(reg, *g)
             if col != EMPTY:
                 if shadow:
@@ -406,6 +554,7 @@ class Walk:
         while not self.in_scene(cr):
             if not self.tick():
                 return 0
+            cr0, o0 = list(cr), so
             hi = wrap32(self.s.D + self.s.min)
             lo = self.s.min
             t = []
@@ -418,16 +567,24 @@ class Walk:
                 return 0
             so = so + d.scale(tMin + EPS)
             cr = [f2i(np.floor(so[i] / F(BLOCK))) for i in range(3)]
+            if cr == cr0 and same(so, o0):
+                self.forever()
+                return 0
         lr = [(so - V(wrap32(cr[0] * BLOCK), wrap32(cr[1] * BLOCK), wrap32(cr[2] * BLOCK))).scale(1.0), d]
         while self.in_scene(cr):
             if not self.tick():
                 return 0
+            cr0, o0 = list(cr), lr[0]
             reg = self.region(cr)
             while reg is None:
                 if not self.tick():
                     return 0
+                cr1, o1 = list(cr), lr[0]
                 self.null_skip(lr, cr, False)
                 if not self.in_scene(cr):
+                    return 0
+                if cr == cr1 and same(lr[0], o1):
+                    self.forever()
                     return 0
                 reg = self.region(cr)
             rwp = self.tr + V(wrap32(cr[0] * BLOCK), wrap32(cr[1] * BLOCK), wrap32(cr[2] * BLOCK))
@@ -437,6 +594,9 @@ class Walk:
             if col != EMPTY:
                 return col
             lr[0] = self.shift_region(cr, lr[0])
+            if cr == cr0 and same(lr[0], o0):
+                self.forever()
+                return 0
         return 0
 
 
@@ -454,8 +614,9 @@ def camera(eye, at, up, fov, aspect):
     return o, llc, u.scale(F(2) * hw), v.scale(F(2) * hh)
 
 
-def render_pixel(scene, lit, cam_fields, W, H, x, y, scale, longest, translation=(0.0, 0.0, 0.0)):
-    """calculateWorldRay + kernel body (Renderer.cuh:1013-1063). cam_fields: (origin, llc, hor, ver) V's."""
+def render_pixel(scene, lit, cam_fields, W, H, x, y, scale, longest, translation=(0.0, 0.0, 0.0), iters=False):
+    """calculateWorldRay + kernel body (Renderer.cuh:1013-1063). cam_fields: (origin, llc, hor, ver) V's.
+    iters: return (colour, loop iterations of the pixel, crawl iterations included)."""
     org, llc, hor, ver = cam_fields
     u = (F(x) + F(0.5)) / F(W)
     v = (F(u32(H - y)) + F(0.5)) / F(H)
@@ -463,4 +624,5 @@ def render_pixel(scene, lit, cam_fields, W, H, x, y, scale, longest, translation
     rd = (ro - org).unit()
     w = Walk(scene, lit, translation)
     col = w.scene(ro, rd, scale, longest)
-    return 0 if w.aborted else col
+    col = 0 if w.aborted else col
+    return (col, w.iters) if iters else col

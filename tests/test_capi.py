@@ -43,7 +43,7 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     assert ctypes.sizeof(_capi.VrCamera) == 60
     assert ctypes.sizeof(_capi.VrLighting) == 44
-    assert ctypes.sizeof(_capi.VrRenderOpts) == 32
+    assert ctypes.sizeof(_capi.VrRenderOpts) == 40
     assert ctypes.sizeof(_capi.VrSynthParams) == 40
 
 

@@ -3,11 +3,15 @@ bit-exact on the packed 0x00RRGGBB words, plus the algorithmic byte count of
 the instrumented kernel against the oracle's count."""
 from __future__ import annotations
 
+import hashlib
+import json
+import os
+
 import numpy as np
 import pytest
 
 import oracle
-from tests.helpers import diff_report, gpu_render, oracle_camera_from, oracle_lighting_from
+from tests.helpers import GOLDEN, diff_report, gpu_render, oracle_camera_from, oracle_lighting_from
 
 pytestmark = pytest.mark.gpu
 
@@ -15,27 +19,45 @@ vr = pytest.importorskip("voxelraymarcher_amd")
 
 STORES = [vr.StorageType.VOXEL_CLUSTER_STORE, vr.StorageType.HASH_TABLE]
 ALGOS = [vr.RayMarchAlgorithm.ORIGINAL, vr.RayMarchAlgorithm.LONGEST_AXIS]
-KERNELS = [vr.Kernel.PERSISTENT, vr.Kernel.TILE]
+KERNELS = [vr.Kernel.TILE]
+FRAMES = {f["name"]: f for f in json.load(open(os.path.join(GOLDEN, "frames.json")))["frames"]}
 
 
 def check_frame(xyz, rgb, store, algo, W, H, scale, cam=None, lit=None, translation=(0.0, 0.0, 0.0),
-                row_begin=0, row_end=None, count=True, oracle_scene=None, gpu_scene=None, kernels=KERNELS):
+                row_begin=0, row_end=None, count=True, oracle_scene=None, gpu_scene=None, kernels=KERNELS,
+                want=None, defer_caps=(0,)):
+    """The GPU frame (every kernel; counted and uncounted; every deferral-list capacity)
+    equals the oracle's pixels and algorithmic bytes.  want = (pixels, bytes) already
+    rendered by the oracle, else rendered here."""
     row_end = H if row_end is None else row_end
     cam = cam or vr.Camera.reference(W, H)
     lit = lit or vr.setup_constant_values()
     info = vr.VoxelSceneInfo(translation, scale)
     scene = gpu_scene or vr.create_scene(xyz, rgb, store)
-    ref = oracle_scene or oracle.Scene(xyz, rgb, int(store))
-    want, obytes = ref.render(int(algo), oracle_camera_from(cam), oracle_lighting_from(lit), W, H, scale,
-                              translation, row_begin, row_end)
+    if want is None:
+        ref = oracle_scene or oracle.Scene(xyz, rgb, int(store))
+        want = ref.render(int(algo), oracle_camera_from(cam), oracle_lighting_from(lit), W, H, scale,
+                          translation, row_begin, row_end)
+    want, obytes = want
     for kernel in kernels:
-        got, gbytes = gpu_render(scene, algo, cam, lit, info, W, H, row_begin, row_end, count=count, kernel=kernel)
-        assert np.array_equal(got, want), f"{kernel.name}: " + diff_report(got, want, W, row_begin)
-        if count:
-            assert gbytes == obytes, f"{kernel.name}: algorithmic bytes: gpu {gbytes} != oracle {obytes}"
-        got2, _ = gpu_render(scene, algo, cam, lit, info, W, H, row_begin, row_end, count=False, kernel=kernel)
-        assert np.array_equal(got2, want), f"{kernel.name} (uncounted): " + diff_report(got2, want, W, row_begin)
+        for cap in defer_caps:
+            tag = f"{kernel.name} defer_cap={cap}"
+            got, gbytes = gpu_render(scene, algo, cam, lit, info, W, H, row_begin, row_end, count=count,
+                                     kernel=kernel, defer_cap=cap)
+            assert np.array_equal(got, want), f"{tag}: " + diff_report(got, want, W, row_begin)
+            if count:
+                assert gbytes == obytes, f"{tag}: algorithmic bytes: gpu {gbytes} != oracle {obytes}"
+            got2, _ = gpu_render(scene, algo, cam, lit, info, W, H, row_begin, row_end, count=False, kernel=kernel,
+                                 defer_cap=cap)
+            assert np.array_equal(got2, want), f"{tag} (uncounted): " + diff_report(got2, want, W, row_begin)
     return want
+
+
+def check_golden(name, img, nbytes):
+    """The frame equals the committed oracle digest (tests/golden/frames.json)."""
+    g = FRAMES[name]
+    assert hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest() == g["sha256"], name
+    assert nbytes == g["algorithmic_bytes"], name
 
 
 @pytest.fixture(scope="module")
@@ -65,49 +87,126 @@ def test_c2_quarter_res(c2, store, algo):
 
 @pytest.mark.parametrize("algo", ALGOS, ids=lambda a: a.name)
 def test_c2_full_res_vcs(c2, algo):
-    """BASELINE configs C2 (original) and C3 (longest axis) at 1920x1080, whole frame."""
+    """BASELINE configs C2 (original) and C3 (longest axis) at 1920x1080, whole frame,
+    against the live oracle and the committed digest."""
     cfg = vr.CONFIGS["C2"]
-    check_frame(*c2, vr.StorageType.VOXEL_CLUSTER_STORE, algo, cfg.width, cfg.height, cfg.scale)
+    want = check_frame(*c2, vr.StorageType.VOXEL_CLUSTER_STORE, algo, cfg.width, cfg.height, cfg.scale)
+    scene = vr.create_scene(*c2, vr.StorageType.VOXEL_CLUSTER_STORE)
+    got, n = gpu_render(scene, algo, vr.Camera.reference(cfg.width, cfg.height), vr.setup_constant_values(),
+                        vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale), cfg.width, cfg.height, count=True)
+    assert np.array_equal(got, want)
+    check_golden("C2" if algo == vr.RayMarchAlgorithm.ORIGINAL else "C3", got, n)
 
 
-def test_c4_dense_hashtable_rows():
-    """C4 (512^3 dense, every region/cluster populated): a band of rows at full width."""
+def test_c4_dense_hashtable_full_frame():
+    """C4 (512^3 dense, every region/cluster populated, ~400 MB cuckoo store): the
+    whole 1920x1080 frame, pixels and algorithmic bytes, live oracle and digest."""
     cfg = vr.CONFIGS["C4"]
     xyz, rgb = cfg.voxels()
     assert len(rgb) > 15_000_000
-    check_frame(xyz, rgb, vr.StorageType.HASH_TABLE, vr.RayMarchAlgorithm.ORIGINAL, cfg.width, cfg.height,
-                cfg.scale, row_begin=500, row_end=532)
+    scene = vr.create_scene(xyz, rgb, vr.StorageType.HASH_TABLE)
+    want = check_frame(xyz, rgb, vr.StorageType.HASH_TABLE, vr.RayMarchAlgorithm.ORIGINAL, cfg.width, cfg.height,
+                       cfg.scale, gpu_scene=scene)
+    check_golden("C4", want, FRAMES["C4"]["algorithmic_bytes"])
+    got, n = gpu_render(scene, vr.RayMarchAlgorithm.ORIGINAL, vr.Camera.reference(cfg.width, cfg.height),
+                        vr.setup_constant_values(), vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale), cfg.width,
+                        cfg.height, count=True)
+    check_golden("C4", got, n)
 
 
-def test_c5_sparse_rows():
-    """C5 (1024^3 sparse, D = 16): rows of the 4K frame, both algorithms."""
+@pytest.fixture(scope="module")
+def c5():
+    """C5 scene on the GPU and in the oracle, and the oracle's full 4K frames (both
+    algorithms; no iteration budget: every cluster-skip crawl runs to its end)."""
     cfg = vr.CONFIGS["C5"]
     xyz, rgb = cfg.voxels()
     g = vr.create_scene(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE)
     o = oracle.Scene(xyz, rgb, 0)
-    assert g.info()["diameter"] == 16
-    for algo in ALGOS:
-        check_frame(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE, algo, cfg.width, cfg.height, cfg.scale,
-                    row_begin=1000, row_end=1016, oracle_scene=o, gpu_scene=g)
+    cam, lit = oracle.reference_camera(cfg.width, cfg.height), oracle.lighting()
+    frames = {a: o.render(int(a), cam, lit, cfg.width, cfg.height, cfg.scale) for a in ALGOS}
+    return cfg, xyz, rgb, g, o, frames
 
 
-def test_c5_crawl_rows():
+@pytest.mark.parametrize("algo", ALGOS, ids=lambda a: a.name)
+def test_c5_full_frame(c5, algo):
+    """C5 (1024^3 sparse, D = 16) at 3840x2160: every pixel and the algorithmic bytes,
+    including ~6 500 (original) / ~4 300 (longest axis) walks of 65 536 to 1.4 million
+    iterations -- cluster-skip crawls that the tile pass hands to the crawl pass."""
+    cfg, xyz, rgb, g, o, frames = c5
+    want = check_frame(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE, algo, cfg.width, cfg.height, cfg.scale,
+                       gpu_scene=g, want=frames[algo])
+    check_golden("C5" if algo == vr.RayMarchAlgorithm.ORIGINAL else "C5-longestaxis", want, frames[algo][1])
+
+
+@pytest.mark.parametrize("algo", ALGOS, ids=lambda a: a.name)
+def test_c5_crawl_rows(c5, algo):
     """C5 rows 696-712: thousands of rays that creep through empty clusters by
-    RN(EPSILON * d) per iteration (o pinned on a cluster plane), most of
-    them until the 65 536-iteration budget -- including a ties-to-even crawl at
-    (792, 709).  The tile pass defers them (with the walk's state at the crawl) and
-    the crawl pass resumes and fast-forwards them;
-    pixels and algorithmic bytes must still equal the oracle's plain walk."""
-    cfg = vr.CONFIGS["C5"]
-    xyz, rgb = cfg.voxels()
-    g = vr.create_scene(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE)
-    o = oracle.Scene(xyz, rgb, 0)
+    RN(EPSILON * d) per iteration (o pinned on a cluster plane) for up to 1.4
+    million iterations -- including a ties-to-even crawl at (792, 709).  The tile pass
+    defers them (original: with the walk's state at the crawl; longest axis: past the
+    tile budget) and the crawl pass fast-forwards them exactly.  TILE_REWALK walks every
+    deferred pixel from its start; defer_cap 64 overflows the deferral list, so the
+    crawl pass finds most pixels by their marker in the frame."""
+    cfg, xyz, rgb, g, o, frames = c5
+    W = cfg.width
+    want = (frames[algo][0][696 * W:712 * W], None)
+    check_frame(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE, algo, cfg.width, cfg.height, cfg.scale,
+                row_begin=696, row_end=712, gpu_scene=g, count=False, want=want,
+                kernels=[vr.Kernel.TILE, vr.Kernel.TILE_REWALK], defer_caps=(0, 64))
+
+
+def test_c5_crawl_pixels_fixture(c5):
+    """The committed longest C5 walks (tests/golden/c5_crawl_pixels.json: oracle colour
+    per pixel, up to 1.4 million iterations) appear in the GPU's 4K frame."""
+    cfg, xyz, rgb, g, o, frames = c5
+    fx = json.load(open(os.path.join(GOLDEN, "c5_crawl_pixels.json")))["pixels"]
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    cam, lit = vr.Camera.reference(cfg.width, cfg.height), vr.setup_constant_values()
     for algo in ALGOS:
-        # TILE resumes each deferred crawl from its record; TILE_REWALK walks the pixel
-        # from its start (the fallback for crawls whose voxel the record cannot pin)
-        check_frame(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE, algo, cfg.width, cfg.height, cfg.scale,
-                    row_begin=696, row_end=712, oracle_scene=o, gpu_scene=g,
-                    kernels=KERNELS + [vr.Kernel.TILE_REWALK])
+        got, _ = gpu_render(g, algo, cam, lit, info, cfg.width, cfg.height, 696, 712)
+        for p in fx:
+            if p["algo"] == int(algo):
+                assert int(got[(p["y"] - 696) * cfg.width + p["x"]]) == p["colour"], p
+
+
+def test_c5_eight_rank_emulation(c5):
+    """C5 as BASELINE defines it -- the fixed 3840x2160 frame cut into 8-row bands dealt
+    round-robin to 8 ranks -- emulated on one GPU: each rank's vr_render_bands buffer,
+    assembled, equals the oracle's frame."""
+    import torch
+
+    from voxelraymarcher_amd.tiles import assemble_bands
+    cfg, xyz, rgb, g, o, frames = c5
+    W, H, R, B = cfg.width, cfg.height, 8, 8
+    cam, lit = vr.Camera.reference(W, H), vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    words = vr.band_buffer_words(W, H, B, R)
+    parts = []
+    for r in range(R):
+        buf = torch.full((words,), -7, dtype=torch.int32, device="cuda")
+        vr.render_bands(g, vr.RayMarchAlgorithm.ORIGINAL, cam, lit, info, W, H, B, r, R, buf)
+        parts.append(buf)
+    torch.cuda.synchronize()
+    img = assemble_bands(torch.stack(parts), W, H, B).cpu().numpy().view(np.uint32).reshape(-1)
+    want = frames[vr.RayMarchAlgorithm.ORIGINAL][0]
+    assert np.array_equal(img, want), diff_report(img, want, W)
+
+
+def test_alias_rays():
+    """Longest-axis rays whose first region probe is outside the region with a `short`
+    cluster id that aliases into the directory (VoxelClusterStore.cuh:21-24,93-99; the
+    kernel's lookup_aliased path): the committed oracle frames (tests/golden/alias_rays.json)."""
+    fx = json.load(open(os.path.join(GOLDEN, "alias_rays.json")))
+    d = np.load(os.path.join(GOLDEN, fx["scene"]))
+    scene = vr.create_scene(d["xyz"], d["rgb"], vr.StorageType.VOXEL_CLUSTER_STORE)
+    lit = vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), fx["scale"])
+    W, H = fx["width"], fx["height"]
+    for c in fx["cameras"]:
+        cam = vr.Camera(c["eye"], c["at"], fx["up"], fx["fov"], fx["aspect"])
+        got, n = gpu_render(scene, vr.RayMarchAlgorithm.LONGEST_AXIS, cam, lit, info, W, H, count=True)
+        assert got.tolist() == c["pixels"], c
+        assert n == c["algorithmic_bytes"], c
 
 
 def test_count_variant_pixels_identical(c2):
@@ -215,3 +314,28 @@ def test_axis_aligned_views(c1, algo):
         cam = vr.Camera(eye, at, up, 20.0, 1.0)
         for store in STORES:
             check_frame(*c1, store, algo, 65, 65, 1, cam=cam)
+
+
+def test_never_ending_walks():
+    """A camera whose rays have NaN directions (plain-data vr_camera: image plane =
+    eye): most walks never finish in the reference (the NaN position repeats the
+    region loop's, entry clip's or cluster skip's state forever).  The tile pass hands
+    them to the crawl pass at its budget; the crawl pass detects the unchanged loop
+    state and writes 0 with 4 bytes, as the oracle does; the one config whose walks
+    do finish renders as usual."""
+    from tests.test_oracle import nan_camera
+    xyz, rgb = vr.CONFIGS["C1"].voxels()
+    cam = vr.Camera.reference(64, 64)
+    for f in ("origin", "lower_left"):
+        for i in range(3):
+            getattr(cam.raw, f)[i] = 1.0
+    for f in ("horizontal", "vertical", "forward"):
+        for i in range(3):
+            getattr(cam.raw, f)[i] = 0.0
+    ocam = nan_camera()
+    lit = vr.setup_constant_values()
+    for store in STORES:
+        ref = oracle.Scene(xyz, rgb, int(store))
+        for algo in ALGOS:
+            want = ref.render(int(algo), ocam, oracle_lighting_from(lit), 64, 64, 12)
+            check_frame(xyz, rgb, store, algo, 64, 64, 12, cam=cam, lit=lit, want=want, defer_caps=(0, 16))

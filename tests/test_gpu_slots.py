@@ -1,9 +1,10 @@
 """GPU test of the per-launch scratch slots (vr_host.cpp SlotRing): the
-crawl-deferral list of a VCS tile launch and the work queue of a persistent
-launch.  Many launches in flight on several streams at once, far more of them
-than the ring has slots, must each render exactly the frame one serial launch
-renders: a slot shared by two launches in flight would mix their deferred
-records (wrong or zero pixels) or their queue heads."""
+crawl pass's deferral list, and the crawl pass's own high-priority stream
+fenced by per-slot events.  Many launches in flight on several streams at
+once, far more of them than the ring has slots, must each render exactly the
+frame one serial launch renders: a slot shared by two launches in flight would
+mix their deferred records (wrong or zero pixels), and a missing fence would
+let a frame be read before its crawl pass wrote it."""
 from __future__ import annotations
 
 import numpy as np
@@ -22,7 +23,7 @@ def c5_scene():
     return cfg, vr.create_scene(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE)
 
 
-@pytest.mark.parametrize("kernel", [vr.Kernel.TILE, vr.Kernel.PERSISTENT], ids=lambda k: k.name)
+@pytest.mark.parametrize("kernel", [vr.Kernel.TILE, vr.Kernel.TILE_REWALK], ids=lambda k: k.name)
 @pytest.mark.parametrize("algo", [vr.RayMarchAlgorithm.ORIGINAL, vr.RayMarchAlgorithm.LONGEST_AXIS],
                          ids=lambda a: a.name)
 def test_launches_in_flight_on_three_streams(c5_scene, kernel, algo):

@@ -161,3 +161,171 @@ def test_scene_geometry_rules():
     sc = oracle.Scene(np.array([[-1, 5, 5], [5, 300, 5]], np.int32), np.array([1, 2], np.uint32), 0)
     assert (sc.min_coord, sc.diameter) == (-1, 6)
     assert sc.region_count == 2
+
+
+# ---------------------------------------------------------------- round 3: walks without a budget
+
+def _cfg_scene(name):
+    """A config's synthetic scene from libvr's host generator (vr_synth_generate,
+    checked against the numpy restatement tests/synth_ref.py in test_capi.py)."""
+    import voxelraymarcher_amd.renderer as R
+    cfg = R.CONFIGS[name]
+    return cfg, cfg.voxels()
+
+
+def test_crawl_run_matches_plain_steps():
+    """pyref.crawl_run (exact rational closed form of a cluster-skip crawl) equals
+    stepping p_i <- RN(p_i + RN(EPSILON * d_i)) one iteration at a time, on random
+    crawls: pinned axis on its cluster's lower plane, positions in every binade of
+    the region, ties-to-even steps included.  (All trials are stepped together.)"""
+    rng = np.random.default_rng(42)
+    F = np.float32
+    P, C, Q, N, LO = [], [], [], [], []
+    for trial in range(1500):
+        lo = [int(v) for v in rng.integers(0, 8, 3) * 8]
+        pin = int(rng.integers(0, 3))
+        d = rng.normal(size=3)
+        d[pin] = -abs(d[pin]) * (10.0 ** -rng.uniform(1.5, 4))    # small negative: EPSILON * d cannot move it
+        d = (d / np.linalg.norm(d)).astype(np.float32)
+        if trial % 7 == 0:                                        # c / ulp = k + 1/2 somewhere
+            d[(pin + 1) % 3] = F(-(2 ** -18) * 1.5 / 1e-4)
+        p = [F(lo[i] + rng.uniform(0, 8) * (rng.uniform() ** 3)) for i in range(3)]
+        p[pin] = F(lo[pin])
+        c = [F(pyref.EPS * F(d[i])) for i in range(3)]
+        if F(p[pin] + c[pin]) != p[pin]:
+            continue
+        n, q = pyref.crawl_run(pyref.V(*p), pyref.V(*d), lo)
+        if not n or n > 20000:            # (the longest batches: test_c5_crawl_pixels_python_restatement)
+            continue
+        P.append(p); C.append(c); Q.append([q[i] for i in range(3)]); N.append(n); LO.append(lo)
+    x, c, n, lo = np.array(P, F), np.array(C, F), np.array(N), np.array(LO, np.float64)
+    assert len(n) > 600
+    for t in range(int(n.max())):
+        act = n > t
+        x[act] = (x[act] + c[act]).astype(F)                      # float32 adds, rounded per step
+        xa = x[act].astype(np.float64)
+        assert ((xa >= lo[act]) & (xa < lo[act] + 8)).all()
+    assert np.array_equal(x, np.array(Q, F))
+
+
+def test_c5_crawl_pixels_python_restatement():
+    """The 100 longest C5 walks per algorithm (rows 696-711, up to 1.4 million
+    iterations; committed in tests/golden/c5_crawl_pixels.json): the plain C oracle
+    (every iteration walked, no budget) and the Python restatement (crawls in exact
+    closed form) agree on colour, iteration count and the committed values."""
+    cfg, (xyz, rgb) = _cfg_scene("C5")
+    fx = json.load(open(os.path.join(GOLDEN, "c5_crawl_pixels.json")))["pixels"]
+    sc = oracle.Scene(xyz, rgb, 0)
+    ps = pyref.Scene(xyz, rgb, 0)
+    W, H = cfg.width, cfg.height
+    cam, lit = oracle.reference_camera(W, H), oracle.lighting()
+    pc = _pyref_camera(cam)
+    for algo in (1, 0):
+        rows = [p for p in fx if p["algo"] == algo]
+        assert len(rows) == 100 and min(p["iterations"] for p in rows) > 100_000
+        px = np.array([p["x"] for p in rows], np.uint32)
+        py = np.array([p["y"] for p in rows], np.uint32)
+        got, b = sc.render_pixels(algo, cam, lit, W, H, cfg.scale, px, py)
+        for i, p in enumerate(rows):
+            assert int(got[i]) == p["colour"] and int(b[i]) == p["bytes"], p
+            col, its = pyref.render_pixel(ps, pyref.Lighting(), pc, W, H, p["x"], p["y"], cfg.scale, algo == 0,
+                                          iters=True)
+            assert (col, its) == (p["colour"], p["iterations"]), (p, col, its)
+
+
+@pytest.mark.parametrize("algo", [oracle.ALGO_ORIGINAL, oracle.ALGO_LONGESTAXIS])
+def test_c2_c3_rays_python_restatement(algo):
+    """120 sampled rays of the C2 (original) / C3 (longest axis) 1920x1080 frame, both stores."""
+    cfg, (xyz, rgb) = _cfg_scene("C2")
+    W, H = cfg.width, cfg.height
+    cam, lit = oracle.reference_camera(W, H), oracle.lighting()
+    rng = np.random.default_rng(7 + algo)
+    px = rng.integers(0, W, 120).astype(np.uint32)
+    py = rng.integers(0, H, 120).astype(np.uint32)
+    for store in (0, 1):
+        sc = oracle.Scene(xyz, rgb, store)
+        ps = pyref.Scene(xyz, rgb, store)
+        got, _ = sc.render_pixels(algo, cam, lit, W, H, cfg.scale, px, py)
+        hits = 0
+        for i in range(len(px)):
+            want = pyref.render_pixel(ps, pyref.Lighting(), _pyref_camera(cam), W, H, int(px[i]), int(py[i]),
+                                      cfg.scale, algo == 0)
+            assert int(got[i]) == want, (store, int(px[i]), int(py[i]))
+            hits += want != 0
+        assert hits > 20
+
+
+def test_alias_rays_python_restatement():
+    """Rays that probe outside their region where the `short` cluster id aliases into
+    the directory (tests/golden/alias_rays.json): the oracle reproduces the committed
+    frames, reports the aliased probes, and the Python restatement agrees on every pixel."""
+    fx = json.load(open(os.path.join(GOLDEN, "alias_rays.json")))
+    d = np.load(os.path.join(GOLDEN, fx["scene"]))
+    sc = oracle.Scene(d["xyz"], d["rgb"], 0)
+    ps = pyref.Scene(d["xyz"], d["rgb"], 0)
+    lit = oracle.lighting()
+    W, H = fx["width"], fx["height"]
+    n_alias = 0
+    for c in fx["cameras"]:
+        cam = oracle.camera(c["eye"], c["at"], fx["up"], fx["fov"], fx["aspect"])
+        img, nbytes = sc.render(0, cam, lit, W, H, 1)
+        assert img.tolist() == c["pixels"] and nbytes == c["algorithmic_bytes"]
+        st = sc.pixel_stats(0, cam, lit, W, H, 1)
+        al = np.flatnonzero(st[..., 8].sum(-1).reshape(-1))
+        assert al.tolist() == c["alias_pixels"]
+        n_alias += len(al)
+        for i in range(W * H):
+            want = pyref.render_pixel(ps, pyref.Lighting(), _pyref_camera(cam), W, H, i % W, i // W, 1, True)
+            assert want == c["pixels"][i], (c["eye"], i)
+    assert n_alias >= 100
+
+
+@pytest.mark.parametrize("name", ["C2", "C3", "C4", "C5", "C5-longestaxis"])
+def test_frame_digests(name):
+    """The oracle's full frames of the GPU configs reproduce the committed digests
+    (tests/golden/frames.json) -- the fixtures the GPU tests check against."""
+    g = {f["name"]: f for f in json.load(open(os.path.join(GOLDEN, "frames.json")))["frames"]}[name]
+    cfg, (xyz, rgb) = _cfg_scene(g["scene"])
+    sc = oracle.Scene(xyz, rgb, g["store"])
+    img, nbytes = sc.render(g["algo"], oracle.reference_camera(g["width"], g["height"]), oracle.lighting(),
+                            g["width"], g["height"], g["scale"])
+    assert hashlib.sha256(img.tobytes()).hexdigest() == g["sha256"]
+    assert nbytes == g["algorithmic_bytes"]
+
+
+def nan_camera():
+    """A camera whose every ray has a NaN direction: image plane = eye (ro - eye = 0,
+    normalize(0) = 0/0).  vr_camera / or_camera are plain data, so a caller can hand
+    the renderer this; the reference's walks then never finish for most scenes: the
+    NaN position keeps floorf(NaN / 64) = 0, so the region loop (or the entry clip, or
+    performVoxelSpaceJump's cluster skip) repeats its state forever."""
+    cam = oracle.OrCamera()
+    for i in range(3):
+        cam.origin[i] = cam.lower_left[i] = 1.0
+        cam.horizontal[i] = cam.vertical[i] = cam.forward[i] = 0.0
+    return cam
+
+
+def test_never_ending_walks():
+    """Walks that never finish render 0 with only the pixel write counted (4 B), in
+    both restatements; walks of the same camera that do finish (the hashtable's
+    longest-axis walk hits a voxel at grid (0,0,1)) are rendered as usual."""
+    xyz, rgb = _golden_scene()
+    cam = nan_camera()
+    pc = (pyref.V(1, 1, 1), pyref.V(1, 1, 1), pyref.V(0, 0, 0), pyref.V(0, 0, 0))
+    ended = 0
+    for store in (0, 1):
+        sc = oracle.Scene(xyz, rgb, store)
+        ps = pyref.Scene(xyz, rgb, store)
+        for algo in (0, 1):
+            img, nbytes = sc.render(algo, cam, oracle.lighting(), 4, 4, 12)
+            assert not img.any()
+            ended += nbytes > 64
+            if not (store == 1 and algo == 0):
+                assert nbytes == 16 * 4, (store, algo)
+            assert pyref.render_pixel(ps, pyref.Lighting(), pc, 4, 4, 1, 2, 12, algo == 0) == 0
+    assert ended == 1
+    # no region at (0,0,0): the entry clip's state repeats
+    sc = oracle.Scene(np.array([[100, 100, 100]], np.int32), np.array([5], np.uint32), 0)
+    img, nbytes = sc.render(1, cam, oracle.lighting(), 4, 4, 1)
+    assert not img.any() and nbytes == 64

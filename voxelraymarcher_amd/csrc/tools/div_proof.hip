@@ -20,6 +20,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "vr_device.h"   // the rcp_setup / div_fast the kernels use: proven as written there
+
 namespace {
 
 constexpr unsigned kDivPerLaunch = 1u << 16;       // divisors per launch
@@ -32,16 +34,14 @@ __global__ __launch_bounds__(256) void prove(unsigned d0, unsigned long long* ba
     const unsigned n0 = (gid % kSplit) * kPerThread;
     const float d = __uint_as_float(0x3F800000u | dm);
     const float ra = 1.0f / d;                                        // RN(1/d)
-    const float r0 = __builtin_amdgcn_rcpf(d);
-    const float rb = __builtin_fmaf(__builtin_fmaf(-d, r0, 1.0f), r0, r0);   // rcp_setup's r
+    const vr::Rcp rc = vr::rcp_setup(d);                              // rcp_setup's r
     unsigned long long la = 0, lb = 0;
     for (unsigned k = 0; k < kPerThread; ++k) {
         const float n = __uint_as_float(0x3F800000u | (n0 + k));
         const float want = n / d;
         float q = n * ra;
         q = __builtin_fmaf(__builtin_fmaf(-d, q, n), ra, q);
-        float p = n * rb;
-        p = __builtin_fmaf(__builtin_fmaf(-d, p, n), rb, p);
+        const float p = vr::div_fast(n, rc);
         const bool ba = __float_as_uint(q) != __float_as_uint(want);
         la += ba;
         lb += __float_as_uint(p) != __float_as_uint(want);
@@ -58,10 +58,7 @@ __global__ __launch_bounds__(256) void prove(unsigned d0, unsigned long long* ba
 __global__ __launch_bounds__(256) void recip_scaling(unsigned long long* bad) {
     const unsigned m = blockIdx.x * blockDim.x + threadIdx.x;       // significand bits
     if (m >= (1u << 23)) return;
-    auto rn = [](float d) {
-        const float r0 = __builtin_amdgcn_rcpf(d);
-        return __builtin_fmaf(__builtin_fmaf(-d, r0, 1.0f), r0, r0);
-    };
+    auto rn = [](float d) { return vr::rcp_setup(d).r; };
     const float r1 = rn(__uint_as_float(0x3F800000u | m));
     unsigned long long local = 0;
     for (int e = -64; e <= 20; ++e) {

@@ -1,5 +1,5 @@
-// vr_device.h -- device-side building blocks shared by the ray-march kernels
-// (vr_march.hip: one lane per pixel; vr_persist.hip: persistent state machine):
+// vr_device.h -- device-side building blocks of the ray-march kernels
+// (vr_march.hip: the tile pass, one lane per pixel, and the crawl pass):
 // math with the reference's operation order, CUDA-semantics conversions,
 // the storage lookups and the lighting.  FP policy: SURVEY.md 8(c).
 #pragma once
@@ -175,8 +175,11 @@ struct Hit {
     bool longest;       // isInShadowRayMarchVoxelSceneLongestAxis vs ...Original
 };
 
-template <int STORE, bool COUNT>
+// BUDGET: kTileBudget (tile pass: aborted = hand the pixel to the crawl pass)
+// or kCrawlBudget (crawl pass: the hang guard).
+template <int STORE, bool COUNT, uint32_t BUDGET>
 struct Ctx {
+    static constexpr uint32_t kBudget = BUDGET;
     const KScene& s;
     const KView& v;
     uint32_t iters = 0;
@@ -190,7 +193,7 @@ struct Ctx {
     }
     __device__ __forceinline__ bool tick() {
         if (aborted) return false;
-        if (++iters > kIterBudget) { aborted = true; return false; }
+        if (++iters > BUDGET) { aborted = true; return false; }
         return true;
     }
 
@@ -404,6 +407,15 @@ struct Ctx {
     // +0 -- so positions stepped from it are never -0 either.
     __device__ __forceinline__ static bool in_region_bits_nz(f3 o) {
         return max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)) < 0x42800000u;
+    }
+    // Loop-state equality for the never-finishes test (crawl pass): the same
+    // bits, or both NaN (every later use treats NaNs alike).
+    __device__ __forceinline__ static bool same_f(float a, float b) {
+        return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
+    }
+    __device__ __forceinline__ static bool same_pos(i3 ca, f3 a, i3 cb, f3 b) {
+        return ca.x == cb.x && ca.y == cb.y && ca.z == cb.z && same_f(a.x, b.x) && same_f(a.y, b.y) &&
+               same_f(a.z, b.z);
     }
     __device__ __forceinline__ static bool grid_in_region(int32_t a, int32_t b, int32_t c) {   // :436-439
         return (uint32_t)a < 64u && (uint32_t)b < 64u && (uint32_t)c < 64u;

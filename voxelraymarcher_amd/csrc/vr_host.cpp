@@ -443,34 +443,88 @@ int make_view(const vr_scene* s, const vr_camera* cam, const vr_lighting* lit, c
     return VR_OK;
 }
 
-// Per-device rings of device scratch slots that a launch borrows: the
-// crawl-deferral list of a tile launch (vr::kDeferWords uint32, zeroed once;
-// the crawl pass resets it at its end) and the work queue of a persistent
-// launch (vr::kQueueWords uint32, zeroed on the launch stream first).  A slot
-// belongs to ONE launch at a time: the launch that takes it waits (on its own
-// stream, hipStreamWaitEvent) for the event the slot's previous launch recorded
-// after its last kernel, and records the slot's event again after its own.  The
-// ring's lock is held from taking the slot to recording the event, so two
-// launches in flight -- on any streams, from any threads -- never share a slot
-// however many slots there are (a wait on an event of the same stream or one
-// that has completed costs nothing).
+// Per-device ring of device scratch slots that a launch borrows: the deferral
+// list of the crawl pass (vr::kDeferWords uint32, zeroed once; the crawl pass
+// resets it at its end).  A slot belongs to ONE launch at a time: the launch
+// that takes it waits (on its own stream, hipStreamWaitEvent) for the event
+// the slot's previous launch recorded after its last kernel, and records the
+// slot's event again after its own.  The device's lock is held from taking the
+// slot to recording the event, so two launches in flight -- on any streams,
+// from any threads -- never share a slot however many slots there are (a wait
+// on an event of the same stream or one that has completed costs nothing).
+// Launches on different devices take different locks.
+//
+// Each device also owns the crawl pass's stream: created with the highest
+// priority the device offers, so the crawl pass's few workgroups are
+// dispatched ahead of the next frame's tile workgroups instead of waiting for
+// CU slots behind them (with two frames in flight the crawl pass
+// on the frame's own stream waited ~60 us for slots).  Per slot, `tile_done`
+// fences it after the tile pass and `crawl_done` fences the caller's stream
+// after it.  VR_CRAWL_STREAM=0 launches the crawl pass on the caller's stream.
 struct SlotRing {
     const char* name;
     size_t words;          // uint32 per slot
     uint32_t nslots;
-    std::mutex mu;
     struct Dev {
+        std::mutex mu;
         uint32_t* base = nullptr;
-        std::vector<hipEvent_t> ev;
+        std::vector<hipEvent_t> ev, tile_done, crawl_done;
         std::vector<bool> used;
+        hipStream_t crawl = nullptr;
         uint32_t next = 0;
     } dev[64];
     SlotRing(const char* n, size_t w, uint32_t s) : name(n), words(w), nslots(s) {}
 };
 SlotRing g_defer_ring("defer ring", vr::kDeferWords, 16);
-SlotRing g_queue_ring("queue ring", vr::kQueueWords, 16);
 
-// The borrowed slot; the lock is held until release() (or destruction).
+bool crawl_stream_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("VR_CRAWL_STREAM");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// First use of a device: the slots, their events and the crawl stream.  On a
+// failure everything made so far is released and the next launch tries again.
+int ring_init(SlotRing& r, SlotRing::Dev& D) {
+    void* q = nullptr;
+    const size_t bytes = (size_t)r.nslots * r.words * sizeof(uint32_t);
+    std::vector<hipEvent_t> made;
+    hipStream_t cs = nullptr;
+    auto undo = [&](hipError_t e, const char* what) {
+        for (hipEvent_t x : made) (void)hipEventDestroy(x);
+        if (cs) (void)hipStreamDestroy(cs);
+        if (q) (void)hipFree(q);
+        return hip_fail(e, what);
+    };
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) { q = nullptr; return undo(e, "hipMalloc(slot ring)"); }
+    e = hipMemset(q, 0, bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) return undo(e, "hipMemset(slot ring)");
+    std::vector<hipEvent_t> ev(r.nslots), td(r.nslots), cd(r.nslots);
+    for (uint32_t i = 0; i < r.nslots; ++i) {
+        for (hipEvent_t* x : {&ev[i], &td[i], &cd[i]}) {
+            e = hipEventCreateWithFlags(x, hipEventDisableTiming);
+            if (e != hipSuccess) return undo(e, "hipEventCreate(slot ring)");
+            made.push_back(*x);
+        }
+    }
+    int lo = 0, hi = 0;
+    e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi);
+    if (e != hipSuccess) { cs = nullptr; return undo(e, "hipStreamCreateWithPriority(crawl stream)"); }
+    D.ev = std::move(ev);
+    D.tile_done = std::move(td);
+    D.crawl_done = std::move(cd);
+    D.used.assign(r.nslots, false);
+    D.crawl = cs;
+    D.base = (uint32_t*)q;
+    return VR_OK;
+}
+
+// The borrowed slot; the device's lock is held until release() (or destruction).
 struct SlotLease {
     SlotRing* ring = nullptr;
     std::unique_lock<std::mutex> lk;
@@ -479,25 +533,13 @@ struct SlotLease {
     uint32_t* p = nullptr;
     int acquire(SlotRing& r, int d, hipStream_t stream) {
         if (d < 0 || d >= 64) return fail(VR_E_INVALID, "device index too large");
-        ring = &r;
-        lk = std::unique_lock<std::mutex>(r.mu);
         SlotRing::Dev& D = r.dev[d];
+        lk = std::unique_lock<std::mutex>(D.mu);
         if (!D.base) {
-            void* q = nullptr;
-            const size_t bytes = (size_t)r.nslots * r.words * sizeof(uint32_t);
-            hipError_t e = hipMalloc(&q, bytes);
-            if (e != hipSuccess) return hip_fail(e, "hipMalloc(slot ring)");
-            e = hipMemset(q, 0, bytes);
-            if (e == hipSuccess) e = hipDeviceSynchronize();
-            if (e != hipSuccess) { (void)hipFree(q); return hip_fail(e, "hipMemset(slot ring)"); }
-            D.ev.assign(r.nslots, nullptr);
-            for (uint32_t i = 0; i < r.nslots; ++i) {
-                e = hipEventCreateWithFlags(&D.ev[i], hipEventDisableTiming);
-                if (e != hipSuccess) return hip_fail(e, "hipEventCreate(slot ring)");
-            }
-            D.used.assign(r.nslots, false);
-            D.base = (uint32_t*)q;
+            int rc = ring_init(r, D);
+            if (rc) return rc;
         }
+        ring = &r;
         dev = d;
         idx = D.next;
         D.next = (D.next + 1u) % r.nslots;
@@ -508,12 +550,12 @@ struct SlotLease {
         p = D.base + r.words * idx;
         return VR_OK;
     }
+    SlotRing::Dev& D() const { return ring->dev[dev]; }
     // after the launch's last kernel on `stream`
     int release(hipStream_t stream) {
-        SlotRing::Dev& D = ring->dev[dev];
-        hipError_t e = hipEventRecord(D.ev[idx], stream);
+        hipError_t e = hipEventRecord(D().ev[idx], stream);
         if (e != hipSuccess) return hip_fail(e, "hipEventRecord(slot ring)");
-        D.used[idx] = true;
+        D().used[idx] = true;
         lk.unlock();
         return VR_OK;
     }
@@ -521,30 +563,31 @@ struct SlotLease {
 
 int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void* stream) {
     if (algo != VR_ALGO_ORIGINAL && algo != VR_ALGO_LONGESTAXIS) return fail(VR_E_INVALID, "unknown algorithm");
+    if (kernel != VR_KERNEL_AUTO && kernel != VR_KERNEL_TILE && kernel != VR_KERNEL_TILE_REWALK)
+        return fail(VR_E_INVALID, "unknown kernel (2, the persistent kernel, was retired)");
     if (v.local_rows == 0 || v.W == 0) return VR_OK;
     DeviceGuard dg(s->device);
     const bool count = v.bytes != nullptr;
     const hipStream_t st = (hipStream_t)stream;
-    hipError_t e;
-    if (kernel == VR_KERNEL_AUTO) kernel = VR_KERNEL_TILE;   // measured fastest for every pair
     v.crawl_rewalk = kernel == VR_KERNEL_TILE_REWALK ? 1u : 0u;
-    if (kernel == VR_KERNEL_TILE_REWALK) kernel = VR_KERNEL_TILE;
+    // the deferral list of the crawl pass (cluster-skip crawls, walks over the tile budget)
     SlotLease lease;
-    if (kernel == VR_KERNEL_TILE) {
-        if (s->store == VR_STORE_VCS) {           // cluster-skip crawls: deferred to a second pass
-            int rc = lease.acquire(g_defer_ring, s->device, st);
-            if (rc) return rc;
-            v.defer = lease.p;
-            v.defer_cap = vr::kDeferCap;
-        }
-        e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st);
-    } else {
-        int rc = lease.acquire(g_queue_ring, s->device, st);
-        if (rc) return rc;
-        e = vr::launch_persist((int)s->store, (int)algo, count, kscene(s), v, lease.p, st);
+    int rc = lease.acquire(g_defer_ring, s->device, st);
+    if (rc) return rc;
+    v.defer = lease.p;
+    v.defer_cap = (v.defer_cap && v.defer_cap < vr::kDeferCap) ? v.defer_cap : vr::kDeferCap;
+    const bool side = crawl_stream_enabled();
+    hipStream_t cs = side ? lease.D().crawl : nullptr;
+    hipEvent_t td = side ? lease.D().tile_done[lease.idx] : nullptr;
+    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st, cs, td);
+    if (e == hipSuccess && side) {
+        // the caller's stream continues after the crawl pass
+        hipEvent_t cd = lease.D().crawl_done[lease.idx];
+        e = hipEventRecord(cd, cs);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, cd, 0);
     }
     // (on a failed launch the slot is still fenced: a kernel of it may be queued)
-    const int rc = lease.ring ? lease.release(st) : VR_OK;
+    rc = lease.release(st);
     if (e != hipSuccess) return hip_fail(e, "ray-march launch");
     return rc;
 }
@@ -841,7 +884,6 @@ int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr
     if (!out_dev) return fail(VR_E_INVALID, "out_dev is NULL");
     if (opts->row_begin > opts->row_end || opts->row_end > height) return fail(VR_E_INVALID, "bad row range");
     if (!opts->nranks || opts->rank >= opts->nranks) return fail(VR_E_INVALID, "bad band partition");
-    if (opts->kernel > VR_KERNEL_TILE_REWALK) return fail(VR_E_INVALID, "unknown kernel");
     const uint32_t rows = opts->row_end - opts->row_begin;
     const uint32_t band = opts->band_rows ? opts->band_rows : std::max(1u, rows);
     v.row0 = opts->row_begin;
@@ -853,13 +895,14 @@ int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr
     v.local_rows = (uint32_t)(vr_band_buffer_words(width, rows, band, opts->nranks) / width);
     v.out = out_dev;
     v.bytes = (unsigned long long*)opts->bytes_dev;
+    v.defer_cap = opts->defer_cap;
     return launch(s, algo, opts->kernel, v, stream);
 }
 
 int vr_render(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit, const float translation[3],
               uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin, uint32_t row_end, uint32_t* out_dev,
               void* stream) {
-    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, nullptr};
+    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, nullptr, 0};
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
@@ -874,7 +917,7 @@ int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t band_rows,
                     uint32_t rank, uint32_t nranks, uint32_t* out_dev, void* stream) {
     if (!band_rows) return fail(VR_E_INVALID, "band_rows must be > 0");
-    vr_render_opts o{VR_KERNEL_AUTO, 0, height, band_rows, rank, nranks, nullptr};
+    vr_render_opts o{VR_KERNEL_AUTO, 0, height, band_rows, rank, nranks, nullptr, 0};
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
@@ -882,7 +925,7 @@ int vr_render_count(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin,
                     uint32_t row_end, uint32_t* out_dev, uint64_t* bytes_dev, void* stream) {
     if (!bytes_dev) return fail(VR_E_INVALID, "bytes_dev is NULL");
-    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, bytes_dev};
+    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, bytes_dev, 0};
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 

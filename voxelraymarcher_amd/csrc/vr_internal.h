@@ -15,7 +15,22 @@ int set_error(int code, const std::string& msg);
 constexpr uint32_t kEmpty = 1u << 30;        // EMPTY_KEY == EMPTY_VAL (VoxelFunctions.cuh:20-21)
 constexpr uint32_t kNone = 0xFFFFFFFFu;      // null region / null cluster in the tables
 constexpr int32_t kBlock = 64;               // BLOCK_SIZE (VoxelFunctions.cuh:24)
-constexpr uint32_t kIterBudget = 65536u;     // per-pixel hang guard
+// Iteration limits ("Walks that never finish").  The walks
+// themselves have no budget: the reference runs every finite walk to its end.
+//  kTileBudget : a tile-pass pixel whose walks exceed this many loop
+//                iterations is handed to the crawl pass and walked there from
+//                its start (normal pixels of every config take < 300; only
+//                cluster-skip crawls run longer).
+//  kCrawlBudget: the crawl pass's hang guard.  Walks that never finish are
+//                detected exactly there (a loop iteration that leaves the
+//                loop's state unchanged); the longest finite walk of any
+//                config takes 1.4e6 iterations, ~770x below this.
+constexpr uint32_t kTileBudget = 4096u;
+constexpr uint32_t kCrawlBudget = 1u << 30;
+// A tile-pass pixel that could not be deferred (the list was full) is written
+// as kDeferMarker (no colour is >= 2^24) and counted in slot word 2; the crawl
+// pass then finds it in the frame.
+constexpr uint32_t kDeferMarker = 0xFFFFFFFFu;
 // VCS walks address a region's cluster masks as a 32-bit byte offset from the
 // scene's mask array (64 KB per occupied 64^3 region): at most 65536 occupied
 // regions (4 GB of masks) per VCS scene; the builders reject larger scenes.
@@ -67,16 +82,18 @@ struct KView {
     uint32_t band_minv;       // floor(2^32 / band_rows) (2^32 - 1 for 1): l / band_rows by a multiply-high
     uint32_t* out;
     unsigned long long* bytes;
-    uint32_t* defer;          // crawl deferral slot: [count, done, 0, 0, records (kDeferRecWords each)...]
+    uint32_t* defer;          // crawl deferral slot: [count, done, overflow, 0, records (kDeferRecWords each)...]
     uint32_t defer_cap;
     uint32_t crawl_rewalk;    // 1: deferred crawls are walked from the pixel's start (VR_KERNEL_TILE_REWALK)
 };
 
 // Rays that start a cluster-skip crawl (see vr_march.hip crawl_steps) in the
-// tile pass are deferred to a second pass over a per-launch list.
-// A slot is [count, done, 0, 0] and kDeferCap records of kDeferRecWords words:
-// the crawling walk's state at the crawl (vr_march.hip, grid_original_rt), from
-// which the crawl pass resumes it.  Record words:
+// tile pass, and pixels that exceed kTileBudget, are deferred to a second pass
+// over a per-launch list.
+// A slot is [count, done, overflow, 0] and kDeferCap records of kDeferRecWords
+// words: the crawling walk's state at the crawl (vr_march.hip, grid_original_rt),
+// from which the crawl pass resumes it, or just the pixel (flag 4: walk it from
+// its start).  Record words:
 //   0 pixel (row << 16 | x)   1 flags (1 shadow walk, 2 longest-axis shadow, 4 walk from the start)
 //   2-4 stepped position      5-7 region         8 unused (0)
 //   9 iterations so far       10 counted bytes so far
@@ -88,14 +105,12 @@ constexpr uint32_t kDeferCap = 16384;
 constexpr uint32_t kDeferRecWords = 20;
 constexpr uint32_t kDeferWords = 4 + kDeferCap * kDeferRecWords;
 
-// Launch one render (defined in vr_march.hip).
+// Launch one render (defined in vr_march.hip): the tile pass on `stream`, the
+// crawl pass on `crawl_stream` fenced by `tile_done` (both may be null: then
+// the crawl pass follows on `stream`).  The caller makes `stream` wait for
+// the crawl pass.
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,
-                        hipStream_t stream);
-// Persistent state-machine kernel (vr_persist.hip); `queue` = kQueueWords
-// uint32 private to this launch (zeroed on the stream before the kernel).
-constexpr uint32_t kQueueWords = 8 * 64;
-hipError_t launch_persist(int store, int algo, bool count, const KScene& s, const KView& v, uint32_t* queue,
-                          hipStream_t stream);
+                        hipStream_t stream, hipStream_t crawl_stream, hipEvent_t tile_done);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);
 
 }  // namespace vr

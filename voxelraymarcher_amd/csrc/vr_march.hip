@@ -176,8 +176,9 @@ constexpr uint32_t kTilesX = VR_TILES_X, kTilesY = VR_TILES_Y;
 // CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
 // crawling ray reserves an entry in the launch's deferral list and unwinds.
 template <int STORE, bool COUNT, bool CRAWL>
-struct Walker : Ctx<STORE, COUNT> {
-    using C = Ctx<STORE, COUNT>;
+struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
+    using C = Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget>;
+    static constexpr uint32_t kBudget = C::kBudget;
     using C::s; using C::v; using C::aborted; using C::tick; using C::exists; using C::lookup;
     using C::lighting; using C::normal_from_t; using C::in_region; using C::grid_in_region;
     using C::advance_region; using C::in_scene; using C::region_at; using C::skip_null; using C::bytes;
@@ -190,6 +191,7 @@ struct Walker : Ctx<STORE, COUNT> {
     // what a deferred crawl must know to be resumed (see the deferral below):
     // bit 1 = the shadow walk is the longest-axis one; the lit colour of the hit
     uint32_t ctx = 0, lit_saved = 0;
+    bool deferred = false;      // tile pass: a crawl record of this pixel was written
 
     // rayMarchVoxelGrid (Renderer.cuh:260-336) and, SHADOW, shadowRayMarchVoxelGrid (:100-172).
     // The cluster-skip step (:290-306) and the voxel step (:318-331) share one
@@ -269,10 +271,10 @@ struct Walker : Ctx<STORE, COUNT> {
             // the stepped position and the iteration budget are folded into a
             // single condition; the step of the hit iteration is computed and
             // discarded (the reference breaks before it).  tick() semantics are
-            // kept: iteration k of the pixel runs iff k <= kIterBudget.
+            // kept: iteration k of the pixel runs iff k <= kBudget.
             o = add(o, f3{0.0f, 0.0f, 0.0f});      // -0 -> +0 (in_region_bits_nz below)
             if (!this->in_region_bits_nz(o)) return false;
-            if (aborted || this->iters >= kIterBudget) { aborted = true; return false; }
+            if (aborted || this->iters >= kBudget) { aborted = true; return false; }
             bool found = false, inside = true, crawl = false;
             // crawl exits (see crawl_steps): from this iteration count on (crawl pass);
             // tile pass: until a deferral failed
@@ -329,9 +331,9 @@ struct Walker : Ctx<STORE, COUNT> {
                         // (Sgn<2>: positive, and the caller checked the reciprocals)
                         constexpr bool kPos = SX == 2 && SY == 2 && SZ == 2;
                         // The iteration count as the budget test reads it, biased so that
-                        // it reaches bits(64.0f) exactly when iters exceeds kIterBudget:
+                        // it reaches bits(64.0f) exactly when iters exceeds kBudget:
                         // one add per iteration.
-                        uint32_t ic = this->iters + (0x42800000u - kIterBudget);
+                        uint32_t ic = this->iters + (0x42800000u - kBudget);
                         VR_DIAG_COUNT((SHADOW ? 4 : 0) + (SX == 0 ? 1 : 0));   // walk entries
                         for (;;) {
                             VR_DIAG_COUNT((SHADOW ? 6 : 2) + (SX == 0 ? 1 : 0));   // loop iterations
@@ -392,7 +394,7 @@ struct Walker : Ctx<STORE, COUNT> {
                                 if (!kPos && __builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
                                     sMin = bad ? am / fabsf(d.x) : sMin;
                                     crawl = bad & walk_ok & skip & (sMin == 0.0f) &
-                                            (CRAWL ? ic + 1u - (0x42800000u - kIterBudget) >= crawl_after : !crawl_off);
+                                            (CRAWL ? ic + 1u - (0x42800000u - kBudget) >= crawl_after : !crawl_off);
                                     if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
                                 }
                             } else {
@@ -405,7 +407,7 @@ struct Walker : Ctx<STORE, COUNT> {
                                     // a skip step with t = 0 (its plane axis has n = 0, so it is
                                     // always on this branch): the ray creeps through an empty cluster
                                     crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
-                                            (CRAWL ? ic + 1u - (0x42800000u - kIterBudget) >= crawl_after : !crawl_off);
+                                            (CRAWL ? ic + 1u - (0x42800000u - kBudget) >= crawl_after : !crawl_off);
                                     if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
                                 }
                                 sMin = fminf(sX, fminf(sY, sZ));
@@ -417,14 +419,14 @@ struct Walker : Ctx<STORE, COUNT> {
                             const float ts = bit_select(fm, -kEps, sMin) + kEps;
                             o = EQ ? add(o, f3{ts * d.x, ts * d.x, ts * d.x}) : add(o, scl(ts, d));
                             // One unsigned compare for hit, region exit (in_region_bits_nz of the
-                            // stepped position) and the budget (iters >= kIterBudget):
+                            // stepped position) and the budget (iters >= kBudget):
                             // (the add as asm: loop strength reduction otherwise keeps two counters)
                             asm("v_add_u32 %0, 1, %0" : "+v"(ic));
                             const uint32_t ev = max(max(max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)),
                                                         ic), fm);
                             if (ev >= 0x42800000u || crawl) break;
                         }
-                        this->iters = ic - (0x42800000u - kIterBudget);
+                        this->iters = ic - (0x42800000u - kBudget);
                     };
                     const uint32_t sg = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
                     using N = Sgn<-1>;
@@ -468,8 +470,8 @@ struct Walker : Ctx<STORE, COUNT> {
                 asm("" : "+v"(blk.x), "+v"(blk.y), "+v"(bit), "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(this->iters));
                 found = !absent(blk) & (__builtin_amdgcn_ubfe(blk.x, bit, 1u) != 0u);
                 inside = found || this->in_region_bits_nz(o);
-                crawl = !found && inside && this->iters < kIterBudget;
-                if (!crawl || !inside || this->iters >= kIterBudget) break;
+                crawl = !found && inside && this->iters < kBudget;
+                if (!crawl || !inside || this->iters >= kBudget) break;
                 if constexpr (!CRAWL) {
                     // Defer only a real crawl: an axis on its own skip plane that
                     // EPSILON * d cannot move (it did not: o is the stepped position),
@@ -503,7 +505,7 @@ struct Walker : Ctx<STORE, COUNT> {
                             // stepped position by the crawl pass: see crawl_kernel)
                             r[1] |= v.crawl_rewalk ? 4u : 0u;
                             r[18] = this->lit_saved;
-                            if (COUNT) this->bytes = 0xFFFFFFFCu;     // + the final 4 = 0
+                            deferred = true;
                             aborted = true;
                             return false;
                         }
@@ -512,7 +514,7 @@ struct Walker : Ctx<STORE, COUNT> {
                 } else {
                     // Off the hot loop: fast-forward the identical crawl iterations
                     // exactly, then resume the walk (no region-entry step).
-                    const Crawl cw = crawl_steps(o, d, qx, qy, qz, px, py, pz, kIterBudget - this->iters);
+                    const Crawl cw = crawl_steps(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters);
                     // declined (binade edge, left the cluster, odd-mantissa tie): a few
                     // plain iterations, then re-arm
                     if (cw.m == 0u) {
@@ -525,7 +527,7 @@ struct Walker : Ctx<STORE, COUNT> {
                         this->iters += cw.m;
                         this->count(4u * cw.m);
                         inside = this->in_region_bits_nz(o);
-                        if (!inside || this->iters >= kIterBudget) break;
+                        if (!inside || this->iters >= kBudget) break;
                     }
                 }
             }
@@ -543,7 +545,7 @@ struct Walker : Ctx<STORE, COUNT> {
             // body ends in one exit test, as in the VCS walk above.
             o = add(o, f3{0.0f, 0.0f, 0.0f});      // -0 -> +0 (in_region_bits_nz below)
             if (!this->in_region_bits_nz(o)) return false;
-            if (aborted || this->iters >= kIterBudget) { aborted = true; return false; }
+            if (aborted || this->iters >= kBudget) { aborted = true; return false; }
             const uint4 m = s.ht_meta[reg];        // {base, M, prime, offset}
             const FastMod fmod = fastmod_setup(m.y);
             const uint2* t1 = s.ht_slots + m.x;
@@ -555,7 +557,7 @@ struct Walker : Ctx<STORE, COUNT> {
             const float nlim = walk_ok ? 0x1p-90f : kInf;
             uint32_t key = 0;
             uint2 e1{0u, 0u}, e2{0u, 0u};
-            uint32_t ic = this->iters + (0x42800000u - kIterBudget);   // biased count (see the VCS walk)
+            uint32_t ic = this->iters + (0x42800000u - kBudget);   // biased count (see the VCS walk)
             for (;;) {
                 const uint32_t vx = (uint32_t)f2i(o.x), vy = (uint32_t)f2i(o.y), vz = (uint32_t)f2i(o.z);
                 key = lshl_or(lshl_or(vx, 10u, vy), 10u, vz);              // generate3DPoint (x<<20|y<<10|z)
@@ -595,7 +597,7 @@ struct Walker : Ctx<STORE, COUNT> {
                 const uint32_t ev = max(max(max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)), ic), fm);
                 if (ev >= 0x42800000u) break;
             }
-            this->iters = ic - (0x42800000u - kIterBudget);
+            this->iters = ic - (0x42800000u - kBudget);
             // why the lane left (see the VCS walk): recomputed from VGPR values
             asm("" : "+v"(e1.x), "+v"(e1.y), "+v"(e2.x), "+v"(e2.y), "+v"(key), "+v"(o.x), "+v"(o.y), "+v"(o.z));
             const bool m1 = e1.x == key, found = m1 || e2.x == key;
@@ -837,7 +839,7 @@ struct Walker : Ctx<STORE, COUNT> {
         // One exit per iteration (each extra exit of a divergent loop costs lane-mask
         // bookkeeping on every iteration): a lane that must leave computes the rest
         // of the iteration on stale values and leaves at its end, with the reason
-        enum : uint32_t { kGo = 0, kHit = 1, kLeft = 2, kBudget = 3, kTail = 4 };
+        enum : uint32_t { kGo = 0, kHit = 1, kLeft = 2, kOver = 3, kTail = 4 };   // kOver: past the budget
         uint32_t why = kGo, it = this->iters;
         VR_DIAG_COUNT(SHADOW ? 19 : 17);               // longest-axis walks
         for (;;) {
@@ -853,7 +855,7 @@ struct Walker : Ctx<STORE, COUNT> {
                 // the loop condition (else the original-DDA tail), then tick()
                 const bool out = !grid_in_region(CL, CM, CS);
                 it += out ? 0u : 1u;
-                ex = out ? kTail : (it > kIterBudget ? kBudget : kGo);
+                ex = out ? kTail : (it > kBudget ? kOver : kGo);
                 const bool hasM = aM != 0, hasS = aS != 0;
                 bool sfirst = false;
                 if (hasM && hasS) {
@@ -868,17 +870,48 @@ struct Walker : Ctx<STORE, COUNT> {
                 AS = mfirst ? gS : CS;
             } else {
                 ++it;                                // tick()
-                ex = it > kIterBudget ? kBudget : kGo;
+                ex = it > kBudget ? kOver : kGo;
                 // performVoxelSpaceJump's cluster skip (:707-725), integer planes from g
                 const int32_t nL = dL > 0.0f ? ((gL / 8) + 1) * 8 : (gL / 8) * 8;
                 const int32_t nM = dM > 0.0f ? ((gM / 8) + 1) * 8 : (gM / 8) * 8;
                 const int32_t nS = dS > 0.0f ? ((gS / 8) + 1) * 8 : (gS / 8) * 8;
                 const auto t = xyz(((float)nL - oL) / dL, ((float)nM - oM) / dM, ((float)nS - oS) / dS);
-                const float tMin = fminf(t.c[0], fminf(t.c[1], t.c[2])) + kEps;
+                const float tm0 = fminf(t.c[0], fminf(t.c[1], t.c[2]));
+                const float tMin = tm0 + kEps;
                 nj = t.c[0] == tMin ? 0u : (t.c[1] == tMin ? 1u : 2u);
+                const float pL = oL, pM = oM, pS = oS;
+                const int32_t qL = gL, qM = gM, qS = gS;
                 oL = oL + tMin * dL; oM = oM + tMin * dM; oS = oS + tMin * dS;
                 gL = f2i(floorf(oL)); gM = f2i(floorf(oM)); gS = f2i(floorf(oS));
                 if (ex == kGo && !grid_in_region(gL, gM, gS)) ex = kLeft;   // left the region: no tail
+                if constexpr (CRAWL) {
+                    if (ex == kGo) {
+                        if (this->same_f(oL, pL) && this->same_f(oM, pM) && this->same_f(oS, pS) && gL == qL &&
+                            gM == qM && gS == qS) {
+                            // the skip changed nothing (a NaN position): the jump loop never ends
+                            ex = kOver;
+                        } else if (tm0 == 0.0f) {
+                            // A jump crawl: an axis pinned on its cluster plane that EPSILON * d
+                            // cannot move, so every skip in this cluster is o += RN(EPSILON * d)
+                            // (tMin = 0 + EPSILON) -- the same recurrence as the original walk's
+                            // crawl: fast-forward it exactly (ticks and existence reads credited;
+                            // the final position stays in the cluster, so the next skip -- whose t
+                            // values a hit's normal reads -- is a plain one).
+                            const f3 on = to_f3(oL, oM, oS), dd = to_f3(dL, dM, dS);
+                            const i3 q = to_i3(qL, qM, qS);
+                            const Crawl cw = crawl_steps(on, dd, q.x, q.y, q.z, dd.x > 0.0f, dd.y > 0.0f, dd.z > 0.0f,
+                                                         kBudget - it);
+                            if (cw.m != 0u) {
+                                const float fm = (float)cw.m;     // m * delta stays inside the binade: exact
+                                const f3 dl{cw.dx, cw.dy, cw.dz};
+                                oL = oL + fm * ax3<PL>(dl); oM = oM + fm * ax3<PM>(dl); oS = oS + fm * ax3<PS>(dl);
+                                gL = f2i(floorf(oL)); gM = f2i(floorf(oM)); gS = f2i(floorf(oS));
+                                it += cw.m;
+                                this->count(4u * cw.m);
+                            }
+                        }
+                    }
+                }
                 CL = gL; CM = gM; CS = gS;
                 AM = gM; AS = gS;
             }
@@ -964,7 +997,7 @@ struct Walker : Ctx<STORE, COUNT> {
             jumping = stop != 3u;                    // jump on / start a jump; CONTINUE_VAL ends one
         }
         this->iters = it;
-        if (why == kBudget) {
+        if (why == kOver) {
             aborted = true;
             return false;
         }
@@ -1045,6 +1078,8 @@ struct Walker : Ctx<STORE, COUNT> {
         while (!in_scene(cr)) {                   // entry clip (:349-373)
             if (!tick()) return false;
             VR_DIAG_COUNT(15);
+            const i3 cr0 = cr;
+            const f3 so0 = so;
             int32_t hi = (int32_t)(s.D + (uint32_t)s.min_coord), lo = s.min_coord;
             int32_t nx = d.x < 0.0f ? hi : lo, ny = d.y < 0.0f ? hi : lo, nz = d.z < 0.0f ? hi : lo;
             const float ax = (float)(nx * kBlock) - so.x, ay = (float)(ny * kBlock) - so.y,
@@ -1066,6 +1101,7 @@ struct Walker : Ctx<STORE, COUNT> {
             if (tMin == kInf) return false;
             so = add(so, scl(tMin + kEps, d));
             cr = i3{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
+            if (CRAWL && this->same_pos(cr, so, cr0, so0)) { aborted = true; return false; }   // never ends
         }
         f3 o = sub(so, mk((float)(cr.x * kBlock), (float)(cr.y * kBlock), (float)(cr.z * kBlock)));
         return primary_regions<ALGO>(o, d, cr, h, nullptr, rc);
@@ -1084,11 +1120,18 @@ struct Walker : Ctx<STORE, COUNT> {
         while (in_scene(cr)) {
             if (!tick()) return false;
             VR_DIAG_COUNT(10);                         // primary region rounds
+            const i3 cr0 = cr;
+            const f3 o0 = o;
             uint32_t reg = region_at(cr);
             while (reg == kNone) {
                 if (!tick()) return false;
                 VR_DIAG_COUNT(11);                     // null-region skips
+                const i3 cr1 = cr;
+                const f3 o1 = o;
                 if (!this->template skip_null<false>(cr, o, d, reg)) return false;
+                // crawl pass: a round that changes nothing repeats forever (the reference never
+                // returns); the tile pass hands such pixels over through its budget
+                if (CRAWL && this->same_pos(cr, o, cr1, o1)) { aborted = true; return false; }
             }
             bool hit = ALGO == ALGO_ORIGINAL ? grid_original<false>(o, d, reg, cr, h, nullptr, rc)
                                              : (STORE == STORE_VCS ? grid_longest_vcs<false>(o, d, reg, cr, h)
@@ -1096,6 +1139,7 @@ struct Walker : Ctx<STORE, COUNT> {
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
+            if (CRAWL && this->same_pos(cr, o, cr0, o0)) { aborted = true; return false; }
         }
         return false;
     }
@@ -1118,11 +1162,16 @@ struct Walker : Ctx<STORE, COUNT> {
         while (in_scene(cr)) {
             if (!tick()) return false;
             VR_DIAG_COUNT(12);                         // shadow region rounds
+            const i3 cr0 = cr;
+            const f3 o0 = o;
             uint32_t reg = region_at(cr);
             while (reg == kNone) {
                 if (!tick()) return false;
                 VR_DIAG_COUNT(13);
+                const i3 cr1 = cr;
+                const f3 o1 = o;
                 if (!this->template skip_null<!LONGEST>(cr, o, d, reg)) return false;
+                if (CRAWL && this->same_pos(cr, o, cr1, o1)) { aborted = true; return false; }   // (as above)
             }
             bool hit = LONGEST ? (STORE == STORE_VCS ? grid_longest_vcs<true>(o, d, reg, cr, dummy)
                                                      : grid_longest<true>(o, d, reg, cr, dummy))
@@ -1130,6 +1179,7 @@ struct Walker : Ctx<STORE, COUNT> {
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
+            if (CRAWL && this->same_pos(cr, o, cr0, o0)) { aborted = true; return false; }
         }
         return false;
     }
@@ -1191,9 +1241,29 @@ __device__ __forceinline__ uint32_t light_and_shadow(Walker<STORE, COUNT, CRAWL>
     return lit * (uint32_t)!sh;
 }
 
+// Tile pass: hand pixel (x, local row l) to the crawl pass, to be walked there
+// from its start (a record with flag 4).  Returns what the tile pass writes for
+// it: 0, or kDeferMarker when the list is full (the crawl pass then finds the
+// pixel by the marker).
+__device__ __forceinline__ uint32_t defer_rewalk(const KView& v, uint32_t x, uint32_t l) {
+    const uint32_t idx = atomicAdd(v.defer, 1u);
+    if (idx < v.defer_cap) {
+        uint32_t* r = v.defer + 4 + (size_t)idx * kDeferRecWords;
+        r[0] = (l << 16) | x;
+        r[1] = 4u;
+        return 0u;
+    }
+    atomicAdd(v.defer + 2, 1u);
+    return kDeferMarker;
+}
+
 // The body of rayMarchSceneOriginal / rayMarchSceneJumpAxis (Renderer.cuh:1033-1063)
-// for pixel (x, local row l): colour, algorithmic bytes (+4 for the pixel write)
-// (a pixel deferred to the crawl pass comes back as 0 with 0 bytes).
+// for pixel (x, local row l): colour, algorithmic bytes (+4 for the pixel write).
+// Tile pass (!CRAWL): a pixel deferred to the crawl pass -- a crawl record, or a
+// walk longer than kTileBudget iterations -- comes back with 0 bytes (the crawl
+// pass writes and counts it).  Crawl pass: a walk that never finishes (the
+// reference would loop forever) is 0 with only the pixel write counted, as in
+// the oracle.
 template <int STORE, int ALGO, bool COUNT, bool CRAWL>
 __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint32_t x, uint32_t l,
                                           uint32_t& bytes) {
@@ -1204,8 +1274,16 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
         Walker<STORE, COUNT, CRAWL> w(s, v);
         Hit h;
         if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
-        if (w.aborted) col = 0;
         bytes = w.bytes + 4u;                     // + the pixel write
+        if (w.aborted) {
+            col = 0;
+            if (CRAWL) {
+                bytes = 4u;
+            } else {
+                bytes = 0u;
+                if (!w.deferred) col = defer_rewalk(v, x, l);
+            }
+        }
     }
     return col;
 }
@@ -1234,8 +1312,11 @@ __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v
         else sh = eq ? w.template shadow<false, true>(o, cr, r) : w.template shadow<false>(o, cr, r);
         col = r[18] * (uint32_t)!sh;
     }
-    if (w.aborted) col = 0;
     bytes = w.bytes + 4u;
+    if (w.aborted) {                              // never finishes (see shade)
+        col = 0;
+        bytes = 4u;
+    }
     return col;
 }
 
@@ -1267,11 +1348,14 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, ALGO == ALGO_ORIGINAL ? VR_
 // exact crawl fast-forward; the last workgroup resets the slot for reuse.
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
-    __shared__ uint32_t n_lds;
-    if (threadIdx.x == 0) n_lds = v.defer[0];
+    __shared__ uint32_t n_lds, ovf_lds;
+    if (threadIdx.x == 0) {
+        n_lds = v.defer[0];
+        ovf_lds = v.defer[2];
+    }
     __syncthreads();
-    const uint32_t total = n_lds;
-    if (total == 0u) return;                  // nothing deferred (the usual case): no reset needed
+    const uint32_t total = n_lds, overflow = ovf_lds;
+    if (total == 0u && overflow == 0u) return;   // nothing deferred (the usual case): no reset needed
     const uint32_t n = min(total, v.defer_cap);
     unsigned long long bytes = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -1301,6 +1385,16 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
                                          : shade_resume<STORE, ALGO, COUNT>(s, v, r, b);
         bytes += b;
     }
+    if (overflow != 0u) {
+        // the list overflowed: the pixels the tile pass could not defer carry the marker
+        const size_t npx = (size_t)v.local_rows * v.W;
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (size_t)gridDim.x * blockDim.x) {
+            if (v.out[i] != kDeferMarker) continue;
+            uint32_t b;
+            v.out[i] = shade<STORE, ALGO, COUNT, true>(s, v, (uint32_t)(i % v.W), (uint32_t)(i / v.W), b);
+            bytes += b;
+        }
+    }
     if (COUNT) add_bytes(v, threadIdx.x & 63u, bytes);
     // Every workgroup has read the count (above) before it adds to `done`; the
     // last one clears the slot for its next launch (ordered by the kernel boundary).
@@ -1308,6 +1402,7 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     if (threadIdx.x == 0 && atomicAdd(&v.defer[1], 1u) == gridDim.x - 1u) {
         v.defer[0] = 0;
         v.defer[1] = 0;
+        v.defer[2] = 0;
     }
 }
 
@@ -1322,17 +1417,29 @@ __global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __rest
 
 }  // namespace
 
-hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream) {
+// The tile pass on `stream`; the crawl pass (a small grid that exits at once
+// when nothing was deferred) on `crawl_stream`, after `tile_done` -- recorded
+// on `stream` behind the tile pass -- when the caller gives one, else on `stream`.
+hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream,
+                        hipStream_t crawl_stream, hipEvent_t tile_done) {
     dim3 grid((v.W + 8u * kTilesX - 1u) / (8u * kTilesX), (v.local_rows + 8u * kTilesY - 1u) / (8u * kTilesY));
     dim3 block(64u * kTilesX * kTilesY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    // VCS walks can crawl: a small crawl-pass grid follows the tile pass
-    // (it exits at once when nothing was deferred).
     const dim3 cgrid(64);
+    hipStream_t cs = stream;
+    auto fence = [&]() {
+        if (crawl_stream && tile_done) {
+            if (hipEventRecord(tile_done, stream) == hipSuccess && hipStreamWaitEvent(crawl_stream, tile_done, 0) == hipSuccess)
+                cs = crawl_stream;
+        }
+    };
 #define VR_LAUNCH(ST, AL, CT)                                                                     \
     do {                                                                                           \
         hipLaunchKernelGGL((march_kernel<ST, AL, CT>), grid, block, 0, stream, s, v);              \
-        if (ST == STORE_VCS && v.defer) hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, block, 0, stream, s, v); \
+        if (v.defer) {                                                                             \
+            fence();                                                                               \
+            hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, block, 0, cs, s, v);             \
+        }                                                                                          \
     } while (0)
     if (store == STORE_VCS) {
         if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, false); }

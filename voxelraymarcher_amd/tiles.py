@@ -38,6 +38,17 @@ def owned_rows(height: int, band_rows: int, rank: int, nranks: int) -> list[int]
     return rows
 
 
+def frame_resolution(width: int, height: int, nranks: int, tiling: str) -> tuple[int, int]:
+    """The frame N ranks render together: "fixed" -- the config's own frame cut into
+    bands over the ranks (BASELINE C5: one 3840x2160 frame tiled over 8 GPUs; strong
+    scaling); "weak" -- the same view at about N x the pixels (weak_scaled_resolution)."""
+    if tiling == "fixed":
+        return width, height
+    if tiling == "weak":
+        return weak_scaled_resolution(width, height, nranks)
+    raise ValueError(f"unknown tiling {tiling!r}")
+
+
 def weak_scaled_resolution(width: int, height: int, nranks: int) -> tuple[int, int]:
     """The same view at about nranks x the pixels (both sides x sqrt(nranks), so the
     aspect ratio -- and with it Camera::Camera's view -- stays put and every rank
