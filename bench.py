@@ -105,34 +105,33 @@ def baseline_threads() -> int:
 
 
 def _oracle_rate(scene, cam, lit, cfg, threads: int, cpu_seconds: float):
-    """Rays per second of the oracle on a bounded sample of the config's frame: evenly
-    spaced 8-row bands (every `stride`-th band; the whole frame when that fits the
-    budget), repeated until about `cpu_seconds` of CPU time (threads x wall) has been
-    spent, after one untimed pass."""
+    """Rays per second of the oracle on a bounded sample of the config's frame: 8-row
+    bands in a fixed order whose every prefix is spread over the whole frame (band
+    97 k mod n for k = 0, 1, ...: a permutation, 97 being prime to the band counts of
+    every config), taken until about `cpu_seconds` of CPU time (threads x wall) has
+    been spent (at least one band), after one untimed band.  Per-band cost varies a lot
+    (C5's crawl rows), so the sample is sized by time, not by a per-ray estimate."""
     W, H = cfg.width, cfg.height
     bands = list(range(0, H, 8))
+    n = len(bands)
+    step = 97 if n % 97 else 89
+    order = [bands[(k * step) % n] for k in range(n)]
 
-    def run(sel):
-        for y in sel:
-            scene.render(int(cfg.algorithm), cam, lit, W, H, cfg.scale, row_begin=y, row_end=min(H, y + 8),
-                         nthreads=threads)
-        return sum(min(H, y + 8) - y for y in sel) * W
+    def band(y):
+        scene.render(int(cfg.algorithm), cam, lit, W, H, cfg.scale, row_begin=y, row_end=min(H, y + 8),
+                     nthreads=threads)
+        return (min(H, y + 8) - y) * W
 
-    # probe 1/64 of the bands to size the sample
+    band(order[0])                                                      # untimed
+    rays, i = 0, 0
     t0 = time.perf_counter()
-    rays = run(bands[::64])
-    per_ray = (time.perf_counter() - t0) * threads / rays
-    stride = max(1, int(np.ceil(per_ray * W * H / cpu_seconds)))
-    sel = bands[::stride]
-    run(sel)                                                           # untimed
-    one = max(per_ray * len(sel) * 8 * W, 1e-3)
-    reps = int(min(60, max(1, np.floor(cpu_seconds / one))))
-    t0 = time.perf_counter()
-    rays = 0
-    for _ in range(reps):
-        rays += run(sel)
-    dt = time.perf_counter() - t0
-    return rays, dt, rays / dt / 1e6, stride
+    while True:
+        rays += band(order[i % len(order)])
+        i += 1
+        dt = time.perf_counter() - t0
+        if dt * threads >= cpu_seconds:
+            break
+    return rays, dt, rays / dt / 1e6, i
 
 
 def cpu_baseline(cfg, xyz, rgb, threads: int) -> dict:
@@ -143,22 +142,25 @@ def cpu_baseline(cfg, xyz, rgb, threads: int) -> dict:
     scene = oracle.Scene(xyz, rgb, int(cfg.store))
     cam = oracle.reference_camera(cfg.width, cfg.height)
     lit = oracle.lighting()
-    rays, dt, rate, stride = _oracle_rate(scene, cam, lit, cfg, threads, 20.0)
-    rays1, dt1, rate1, stride1 = _oracle_rate(scene, cam, lit, cfg, 1, 6.0)
+    rays, dt, rate, nbands = _oracle_rate(scene, cam, lit, cfg, threads, 20.0)
+    rays1, dt1, rate1, nbands1 = _oracle_rate(scene, cam, lit, cfg, 1, 6.0)
     ci = cpu_info()
 
-    def sample(r, s, t, n):
-        part = "the whole frame" if s == 1 else f"every {s}th 8-row band of the frame"
-        return (f"{r} primary rays of {cfg.name} ({part}, repeated) in {t:.2f} s wall on {n} thread(s) "
-                f"({t * n:.1f} CPU-s), oracle/vr_oracle.c -O3 OpenMP")
+    nb = -(-cfg.height // 8)
+
+    def sample(r, k, t, n):
+        part = (f"{k} of its {nb} 8-row bands, spread evenly" if k < nb else
+                f"the whole frame x{k / nb:.2f}")
+        return (f"{r} primary rays of {cfg.name} {cfg.width}x{cfg.height} ({part}) in {t:.2f} s wall on {n} "
+                f"thread(s) ({t * n:.1f} CPU-s), oracle/vr_oracle.c -O3 OpenMP")
 
     return {"value": round(rate, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": sample(rays, stride, dt, threads),
+            "sample": sample(rays, nbands, dt, threads),
             "cpu_model": ci.get("model"), "machine_cpus": ci.get("machine_cpus"),
             "threads_note": "all CPUs of this process's affinity mask, capped by OMP_NUM_THREADS (the GPU "
                             "box's CPU share); machine_cpus is the whole host",
             "single_core": {"value": round(rate1, 3), "unit": "Mrays/s", "cores": 1,
-                            "sample": sample(rays1, stride1, dt1, 1)}}
+                            "sample": sample(rays1, nbands1, dt1, 1)}}
 
 
 def load_traffic(path: str, cfg_name: str, world: int) -> dict:

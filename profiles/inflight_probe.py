@@ -4,7 +4,7 @@
 device synchronisation.  S = 1 is the serial frame loop; S > 1 lets the tail of
 frame i (a few long waves) overlap the start of frame i+1.  Prints frames/s,
 Mrays/s and whether every frame equals the serial frame.
-  python profiles/inflight_probe.py [C2] [K] [tile|persistent]"""
+  python profiles/inflight_probe.py [C2] [K] [tile|rewalk]"""
 import os
 import sys
 import time
@@ -16,7 +16,7 @@ import voxelraymarcher_amd as vr  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "C2"
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 60
-kern = {"tile": vr.Kernel.TILE, "persistent": vr.Kernel.PERSISTENT}[sys.argv[3] if len(sys.argv) > 3 else "tile"]
+kern = {"tile": vr.Kernel.TILE, "rewalk": vr.Kernel.TILE_REWALK}[sys.argv[3] if len(sys.argv) > 3 else "tile"]
 cfg = vr.CONFIGS[name]
 xyz, rgb = cfg.voxels()
 scene = vr.create_scene(xyz, rgb, cfg.store)

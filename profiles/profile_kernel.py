@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Profiling driver: render one BASELINE config `--iters` times (kernel only,
 inputs resident), printing the HIP-event average per launch.  Run under
-rocprofv3 by profiles/run_rocprof.sh."""
+rocprofv3 by profiles/r03/profile_round.sh."""
 import argparse
 import os
 import sys
@@ -18,9 +18,9 @@ p.add_argument("--iters", type=int, default=20)
 p.add_argument("--no-shadows", action="store_true")
 p.add_argument("--algo", choices=["original", "longestaxis"], default=None)
 p.add_argument("--store", choices=["vcs", "hashtable"], default=None)
-p.add_argument("--kernel", choices=["auto", "persistent", "tile"], default="auto")
+p.add_argument("--kernel", choices=["auto", "tile", "rewalk"], default="auto")
 a = p.parse_args()
-kern = {"auto": vr.Kernel.AUTO, "tile": vr.Kernel.TILE, "persistent": vr.Kernel.PERSISTENT}[a.kernel]
+kern = {"auto": vr.Kernel.AUTO, "tile": vr.Kernel.TILE, "rewalk": vr.Kernel.TILE_REWALK}[a.kernel]
 cfg = vr.CONFIGS[a.config]
 store = cfg.store if a.store is None else vr.parse_storage(a.store)
 algo = cfg.algorithm if a.algo is None else vr.parse_algorithm(a.algo)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarize a run_rocprof.sh output directory: per-kernel mean duration and
-per-dispatch mean of every PMC counter (march/persist kernels only)."""
+per-dispatch mean of every PMC counter (march kernels only)."""
 import collections
 import csv
 import glob
@@ -17,7 +17,7 @@ def summarize(d):
     agg = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "pmc_*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "march_kernel" in r["Kernel_Name"] or "persist_kernel" in r["Kernel_Name"]:
+            if "march_kernel" in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
                 out["vgpr"] = r.get("VGPR_Count")
                 out["sgpr"] = r.get("SGPR_Count")

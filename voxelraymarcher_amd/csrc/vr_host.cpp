@@ -453,14 +453,7 @@ int make_view(const vr_scene* s, const vr_camera* cam, const vr_lighting* lit, c
 // from any threads -- never share a slot however many slots there are (a wait
 // on an event of the same stream or one that has completed costs nothing).
 // Launches on different devices take different locks.
-//
-// Each device also owns the crawl pass's stream: created with the highest
-// priority the device offers, so the crawl pass's few workgroups are
-// dispatched ahead of the next frame's tile workgroups instead of waiting for
-// CU slots behind them (with two frames in flight the crawl pass
-// on the frame's own stream waited ~60 us for slots).  Per slot, `tile_done`
-// fences it after the tile pass and `crawl_done` fences the caller's stream
-// after it.  VR_CRAWL_STREAM=0 launches the crawl pass on the caller's stream.
+
 struct SlotRing {
     const char* name;
     size_t words;          // uint32 per slot
@@ -468,33 +461,22 @@ struct SlotRing {
     struct Dev {
         std::mutex mu;
         uint32_t* base = nullptr;
-        std::vector<hipEvent_t> ev, tile_done, crawl_done;
+        std::vector<hipEvent_t> ev;
         std::vector<bool> used;
-        hipStream_t crawl = nullptr;
         uint32_t next = 0;
     } dev[64];
     SlotRing(const char* n, size_t w, uint32_t s) : name(n), words(w), nslots(s) {}
 };
 SlotRing g_defer_ring("defer ring", vr::kDeferWords, 16);
 
-bool crawl_stream_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("VR_CRAWL_STREAM");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// First use of a device: the slots, their events and the crawl stream.  On a
+// First use of a device: the slots and their events.  On a
 // failure everything made so far is released and the next launch tries again.
 int ring_init(SlotRing& r, SlotRing::Dev& D) {
     void* q = nullptr;
     const size_t bytes = (size_t)r.nslots * r.words * sizeof(uint32_t);
     std::vector<hipEvent_t> made;
-    hipStream_t cs = nullptr;
     auto undo = [&](hipError_t e, const char* what) {
         for (hipEvent_t x : made) (void)hipEventDestroy(x);
-        if (cs) (void)hipStreamDestroy(cs);
         if (q) (void)hipFree(q);
         return hip_fail(e, what);
     };
@@ -503,23 +485,14 @@ int ring_init(SlotRing& r, SlotRing::Dev& D) {
     e = hipMemset(q, 0, bytes);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) return undo(e, "hipMemset(slot ring)");
-    std::vector<hipEvent_t> ev(r.nslots), td(r.nslots), cd(r.nslots);
+    std::vector<hipEvent_t> ev(r.nslots);
     for (uint32_t i = 0; i < r.nslots; ++i) {
-        for (hipEvent_t* x : {&ev[i], &td[i], &cd[i]}) {
-            e = hipEventCreateWithFlags(x, hipEventDisableTiming);
-            if (e != hipSuccess) return undo(e, "hipEventCreate(slot ring)");
-            made.push_back(*x);
-        }
+        e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+        if (e != hipSuccess) return undo(e, "hipEventCreate(slot ring)");
+        made.push_back(ev[i]);
     }
-    int lo = 0, hi = 0;
-    e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi);
-    if (e != hipSuccess) { cs = nullptr; return undo(e, "hipStreamCreateWithPriority(crawl stream)"); }
     D.ev = std::move(ev);
-    D.tile_done = std::move(td);
-    D.crawl_done = std::move(cd);
     D.used.assign(r.nslots, false);
-    D.crawl = cs;
     D.base = (uint32_t*)q;
     return VR_OK;
 }
@@ -576,16 +549,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void*
     if (rc) return rc;
     v.defer = lease.p;
     v.defer_cap = (v.defer_cap && v.defer_cap < vr::kDeferCap) ? v.defer_cap : vr::kDeferCap;
-    const bool side = crawl_stream_enabled();
-    hipStream_t cs = side ? lease.D().crawl : nullptr;
-    hipEvent_t td = side ? lease.D().tile_done[lease.idx] : nullptr;
-    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st, cs, td);
-    if (e == hipSuccess && side) {
-        // the caller's stream continues after the crawl pass
-        hipEvent_t cd = lease.D().crawl_done[lease.idx];
-        e = hipEventRecord(cd, cs);
-        if (e == hipSuccess) e = hipStreamWaitEvent(st, cd, 0);
-    }
+    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st);
     // (on a failed launch the slot is still fenced: a kernel of it may be queued)
     rc = lease.release(st);
     if (e != hipSuccess) return hip_fail(e, "ray-march launch");

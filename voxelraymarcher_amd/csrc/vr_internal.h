@@ -105,12 +105,9 @@ constexpr uint32_t kDeferCap = 16384;
 constexpr uint32_t kDeferRecWords = 20;
 constexpr uint32_t kDeferWords = 4 + kDeferCap * kDeferRecWords;
 
-// Launch one render (defined in vr_march.hip): the tile pass on `stream`, the
-// crawl pass on `crawl_stream` fenced by `tile_done` (both may be null: then
-// the crawl pass follows on `stream`).  The caller makes `stream` wait for
-// the crawl pass.
+// Launch one render (defined in vr_march.hip): the tile pass and the crawl pass on `stream`.
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,
-                        hipStream_t stream, hipStream_t crawl_stream, hipEvent_t tile_done);
+                        hipStream_t stream);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);
 
 }  // namespace vr

@@ -107,6 +107,48 @@ __device__ __forceinline__ Crawl crawl_steps(f3 on, f3 d, int32_t vx, int32_t vy
     return r;
 }
 
+// A whole crawl through one cluster (crawl pass): from `o` -- the position a crawl
+// iteration stepped to from voxel q -- apply every further crawl iteration whose
+// result stays in q's cluster: runs of identical steps in one binade at once
+// (crawl_steps), and the steps between runs (across a binade edge, a tie from an
+// odd mantissa) one by one, exactly as the walk computes them, o_i + RN(EPSILON *
+// d_i).  Returns their number (0: not a crawl, or the next step leaves the
+// cluster); at most `room`.  The step that leaves the cluster is left to the walk
+// (performVoxelSpaceJump's hit normal reads its t values).  Pure arithmetic: a
+// crawl of 10^5..10^6 iterations costs a few dozen loop trips instead of as many
+// dependent mask loads.
+__device__ __forceinline__ uint32_t crawl_run(f3& o, f3 d, int32_t qx, int32_t qy, int32_t qz, bool px, bool py,
+                                              bool pz, uint32_t room) {
+    const f3 c{kEps * d.x, kEps * d.y, kEps * d.z};
+    const int32_t lx = qx & ~7, ly = qy & ~7, lz = qz & ~7;
+    // an axis pinned on its cluster plane: direction negative, on the plane, unmoved by its step
+    const bool pinned = (!px && (float)lx == o.x && o.x + c.x == o.x) ||
+                        (!py && (float)ly == o.y && o.y + c.y == o.y) ||
+                        (!pz && (float)lz == o.z && o.z + c.z == o.z);
+    if (!pinned) return 0u;
+    auto inside = [&](f3 p) {   // in the cluster [l, l + 8) on every axis (p >= 0: trunc = floor)
+        return p.x >= (float)lx && p.x < (float)(lx + 8) && p.y >= (float)ly && p.y < (float)(ly + 8) &&
+               p.z >= (float)lz && p.z < (float)(lz + 8);
+    };
+    if (!inside(o)) return 0u;                  // the crawl iteration itself left the cluster
+    uint32_t n = 0;
+#pragma unroll 1
+    for (uint32_t trip = 0; trip < 4096u && n < room; ++trip) {
+        const Crawl cw = crawl_steps(o, d, qx, qy, qz, px, py, pz, room - n);
+        if (cw.m != 0u) {
+            const float fm = (float)cw.m;       // exact: m * delta_i stays inside the binade
+            o = f3{o.x + fm * cw.dx, o.y + fm * cw.dy, o.z + fm * cw.dz};
+            n += cw.m;
+            if (n >= room) break;
+        }
+        const f3 o1{o.x + c.x, o.y + c.y, o.z + c.z};
+        if (!inside(o1)) break;
+        o = o1;
+        ++n;
+    }
+    return n;
+}
+
 // Direction-sign specialisation of the VCS loop: S = +1 / -1 a sign every lane
 // of the wave shares, 0 = per lane.  plane_v is px ? ceilf(o) + EPSILON :
 // floorf(o) - EPSILON (next_plane_fma's value); plane_c8 the cluster-skip offset.
@@ -173,11 +215,24 @@ constexpr uint32_t kTilesX = VR_TILES_X, kTilesY = VR_TILES_Y;
 #define VR_LONG_TAIL_GENERIC false
 #endif
 
+// The iteration count of a tile-pass walk that wrote a crawl record (see the deferral
+// in grid_original_rt): the pixel is the crawl pass's already.
+constexpr uint32_t kDeferredIters = 0xFFFFFFFFu;
+
 // CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
 // crawling ray reserves an entry in the launch's deferral list and unwinds.
+// kExact (the crawl pass): every walk runs to its end here, and a loop round that
+// leaves its state unchanged is detected as a walk that never finishes.  Otherwise
+// (the tile pass) a walk past kTileBudget iterations is handed to the crawl pass.
+// (Making the cuckoo store's tile pass exact instead -- it has no cluster skips, so
+// no crawls, and could do without a crawl pass -- keeps the round-state snapshot live
+// through its walk loop: C4 0.085 -> 0.109 ms per frame, profiles/r03/ab_exact_cuckoo.txt.)
+template <int STORE, bool CRAWL>
+struct ExactWalk { static constexpr bool value = CRAWL; };
 template <int STORE, bool COUNT, bool CRAWL>
-struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
-    using C = Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget>;
+struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget : kTileBudget> {
+    using C = Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget : kTileBudget>;
+    static constexpr bool kExact = ExactWalk<STORE, CRAWL>::value;
     static constexpr uint32_t kBudget = C::kBudget;
     using C::s; using C::v; using C::aborted; using C::tick; using C::exists; using C::lookup;
     using C::lighting; using C::normal_from_t; using C::in_region; using C::grid_in_region;
@@ -191,7 +246,6 @@ struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
     // what a deferred crawl must know to be resumed (see the deferral below):
     // bit 1 = the shadow walk is the longest-axis one; the lit colour of the hit
     uint32_t ctx = 0, lit_saved = 0;
-    bool deferred = false;      // tile pass: a crawl record of this pixel was written
 
     // rayMarchVoxelGrid (Renderer.cuh:260-336) and, SHADOW, shadowRayMarchVoxelGrid (:100-172).
     // The cluster-skip step (:290-306) and the voxel step (:318-331) share one
@@ -505,7 +559,9 @@ struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
                             // stepped position by the crawl pass: see crawl_kernel)
                             r[1] |= v.crawl_rewalk ? 4u : 0u;
                             r[18] = this->lit_saved;
-                            deferred = true;
+                            // (the flag that the record exists is this sentinel: a bool here would
+                            // be carried through every loop as a lane mask -- SGPR spills)
+                            this->iters = kDeferredIters;
                             aborted = true;
                             return false;
                         }
@@ -514,18 +570,14 @@ struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
                 } else {
                     // Off the hot loop: fast-forward the identical crawl iterations
                     // exactly, then resume the walk (no region-entry step).
-                    const Crawl cw = crawl_steps(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters);
-                    // declined (binade edge, left the cluster, odd-mantissa tie): a few
-                    // plain iterations, then re-arm
-                    if (cw.m == 0u) {
+                    const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters);
+                    // none (not a real crawl, or its next step leaves the cluster): a few plain
+                    // iterations, then re-arm
+                    if (n == 0u) {
                         crawl_after = this->iters + 8u;
                     } else {
-                        const float fm = (float)cw.m;       // exact: m * delta_i stays inside the binade
-                        o.x = o.x + fm * cw.dx;
-                        o.y = o.y + fm * cw.dy;
-                        o.z = o.z + fm * cw.dz;
-                        this->iters += cw.m;
-                        this->count(4u * cw.m);
+                        this->iters += n;
+                        this->count(4u * n);
                         inside = this->in_region_bits_nz(o);
                         if (!inside || this->iters >= kBudget) break;
                     }
@@ -897,17 +949,16 @@ struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
                             // crawl: fast-forward it exactly (ticks and existence reads credited;
                             // the final position stays in the cluster, so the next skip -- whose t
                             // values a hit's normal reads -- is a plain one).
-                            const f3 on = to_f3(oL, oM, oS), dd = to_f3(dL, dM, dS);
+                            f3 on = to_f3(oL, oM, oS);
+                            const f3 dd = to_f3(dL, dM, dS);
                             const i3 q = to_i3(qL, qM, qS);
-                            const Crawl cw = crawl_steps(on, dd, q.x, q.y, q.z, dd.x > 0.0f, dd.y > 0.0f, dd.z > 0.0f,
+                            const uint32_t n = crawl_run(on, dd, q.x, q.y, q.z, dd.x > 0.0f, dd.y > 0.0f, dd.z > 0.0f,
                                                          kBudget - it);
-                            if (cw.m != 0u) {
-                                const float fm = (float)cw.m;     // m * delta stays inside the binade: exact
-                                const f3 dl{cw.dx, cw.dy, cw.dz};
-                                oL = oL + fm * ax3<PL>(dl); oM = oM + fm * ax3<PM>(dl); oS = oS + fm * ax3<PS>(dl);
+                            if (n != 0u) {
+                                oL = ax3<PL>(on); oM = ax3<PM>(on); oS = ax3<PS>(on);
                                 gL = f2i(floorf(oL)); gM = f2i(floorf(oM)); gS = f2i(floorf(oS));
-                                it += cw.m;
-                                this->count(4u * cw.m);
+                                it += n;
+                                this->count(4u * n);
                             }
                         }
                     }
@@ -1101,7 +1152,7 @@ struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
             if (tMin == kInf) return false;
             so = add(so, scl(tMin + kEps, d));
             cr = i3{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
-            if (CRAWL && this->same_pos(cr, so, cr0, so0)) { aborted = true; return false; }   // never ends
+            if (kExact && this->same_pos(cr, so, cr0, so0)) { aborted = true; return false; }   // never ends
         }
         f3 o = sub(so, mk((float)(cr.x * kBlock), (float)(cr.y * kBlock), (float)(cr.z * kBlock)));
         return primary_regions<ALGO>(o, d, cr, h, nullptr, rc);
@@ -1129,9 +1180,9 @@ struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
                 const i3 cr1 = cr;
                 const f3 o1 = o;
                 if (!this->template skip_null<false>(cr, o, d, reg)) return false;
-                // crawl pass: a round that changes nothing repeats forever (the reference never
-                // returns); the tile pass hands such pixels over through its budget
-                if (CRAWL && this->same_pos(cr, o, cr1, o1)) { aborted = true; return false; }
+                // kExact: a round that changes nothing repeats forever (the reference never
+                // returns); the VCS tile pass hands such pixels over through its budget
+                if (kExact && this->same_pos(cr, o, cr1, o1)) { aborted = true; return false; }
             }
             bool hit = ALGO == ALGO_ORIGINAL ? grid_original<false>(o, d, reg, cr, h, nullptr, rc)
                                              : (STORE == STORE_VCS ? grid_longest_vcs<false>(o, d, reg, cr, h)
@@ -1139,7 +1190,7 @@ struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
-            if (CRAWL && this->same_pos(cr, o, cr0, o0)) { aborted = true; return false; }
+            if (kExact && this->same_pos(cr, o, cr0, o0)) { aborted = true; return false; }
         }
         return false;
     }
@@ -1171,7 +1222,7 @@ struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
                 const i3 cr1 = cr;
                 const f3 o1 = o;
                 if (!this->template skip_null<!LONGEST>(cr, o, d, reg)) return false;
-                if (CRAWL && this->same_pos(cr, o, cr1, o1)) { aborted = true; return false; }   // (as above)
+                if (kExact && this->same_pos(cr, o, cr1, o1)) { aborted = true; return false; }   // (as above)
             }
             bool hit = LONGEST ? (STORE == STORE_VCS ? grid_longest_vcs<true>(o, d, reg, cr, dummy)
                                                      : grid_longest<true>(o, d, reg, cr, dummy))
@@ -1179,7 +1230,7 @@ struct Walker : Ctx<STORE, COUNT, CRAWL ? kCrawlBudget : kTileBudget> {
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
-            if (CRAWL && this->same_pos(cr, o, cr0, o0)) { aborted = true; return false; }
+            if (kExact && this->same_pos(cr, o, cr0, o0)) { aborted = true; return false; }
         }
         return false;
     }
@@ -1277,11 +1328,11 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
         bytes = w.bytes + 4u;                     // + the pixel write
         if (w.aborted) {
             col = 0;
-            if (CRAWL) {
+            if (Walker<STORE, COUNT, CRAWL>::kExact) {
                 bytes = 4u;
             } else {
                 bytes = 0u;
-                if (!w.deferred) col = defer_rewalk(v, x, l);
+                if (w.iters != kDeferredIters) col = defer_rewalk(v, x, l);
             }
         }
     }
@@ -1417,29 +1468,22 @@ __global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __rest
 
 }  // namespace
 
-// The tile pass on `stream`; the crawl pass (a small grid that exits at once
-// when nothing was deferred) on `crawl_stream`, after `tile_done` -- recorded
-// on `stream` behind the tile pass -- when the caller gives one, else on `stream`.
-hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream,
-                        hipStream_t crawl_stream, hipEvent_t tile_done) {
+// The tile pass, then the crawl pass (a small grid that exits at once when nothing
+// was deferred), both on `stream`.  (The crawl pass on a high-priority side stream,
+// fenced by events, measured slower on every config: C2 0.1148 -> 0.1224 ms per frame
+// with two in flight, 0.154 -> 0.184 alone; profiles/r03/ab_crawl_stream.txt.)
+hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream) {
     dim3 grid((v.W + 8u * kTilesX - 1u) / (8u * kTilesX), (v.local_rows + 8u * kTilesY - 1u) / (8u * kTilesY));
     dim3 block(64u * kTilesX * kTilesY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    const dim3 cgrid(64);
-    hipStream_t cs = stream;
-    auto fence = [&]() {
-        if (crawl_stream && tile_done) {
-            if (hipEventRecord(tile_done, stream) == hipSuccess && hipStreamWaitEvent(crawl_stream, tile_done, 0) == hipSuccess)
-                cs = crawl_stream;
-        }
-    };
+#ifndef VR_CRAWL_WGS
+#define VR_CRAWL_WGS 64
+#endif
+    const dim3 cgrid(VR_CRAWL_WGS);
 #define VR_LAUNCH(ST, AL, CT)                                                                     \
     do {                                                                                           \
         hipLaunchKernelGGL((march_kernel<ST, AL, CT>), grid, block, 0, stream, s, v);              \
-        if (v.defer) {                                                                             \
-            fence();                                                                               \
-            hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, block, 0, cs, s, v);             \
-        }                                                                                          \
+        if (v.defer) hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, block, 0, stream, s, v); \
     } while (0)
     if (store == STORE_VCS) {
         if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, false); }
