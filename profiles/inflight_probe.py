@@ -15,9 +15,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import voxelraymarcher_amd as vr  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "C2"
+name, _, algo_override = name.partition(":")      # e.g. C5:longestaxis
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 60
 kern = {"tile": vr.Kernel.TILE, "rewalk": vr.Kernel.TILE_REWALK}[sys.argv[3] if len(sys.argv) > 3 else "tile"]
 cfg = vr.CONFIGS[name]
+if algo_override:
+    import dataclasses
+    cfg = dataclasses.replace(cfg, algorithm=vr.parse_algorithm(algo_override))
 xyz, rgb = cfg.voxels()
 scene = vr.create_scene(xyz, rgb, cfg.store)
 W, H = cfg.width, cfg.height

@@ -464,6 +464,8 @@ struct SlotRing {
         std::vector<hipEvent_t> ev;
         std::vector<bool> used;
         uint32_t next = 0;
+        uint32_t* stat_host = nullptr;     // host-mapped: the last crawl pass's record count
+        uint32_t* stat_dev = nullptr;
     } dev[64];
     SlotRing(const char* n, size_t w, uint32_t s) : name(n), words(w), nslots(s) {}
 };
@@ -491,8 +493,19 @@ int ring_init(SlotRing& r, SlotRing::Dev& D) {
         if (e != hipSuccess) return undo(e, "hipEventCreate(slot ring)");
         made.push_back(ev[i]);
     }
+    void* h = nullptr;
+    void* hd = nullptr;
+    e = hipHostMalloc(&h, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+        *(volatile uint32_t*)h = 0u;
+        e = hipHostGetDevicePointer(&hd, h, 0);
+        if (e != hipSuccess) (void)hipHostFree(h);
+    }
+    if (e != hipSuccess) return undo(e, "hipHostMalloc(crawl statistics)");
     D.ev = std::move(ev);
     D.used.assign(r.nslots, false);
+    D.stat_host = (uint32_t*)h;
+    D.stat_dev = (uint32_t*)hd;
     D.base = (uint32_t*)q;
     return VR_OK;
 }
@@ -549,7 +562,9 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void*
     if (rc) return rc;
     v.defer = lease.p;
     v.defer_cap = (v.defer_cap && v.defer_cap < vr::kDeferCap) ? v.defer_cap : vr::kDeferCap;
-    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st);
+    v.defer_stat = lease.D().stat_dev;
+    const uint32_t expect = *(volatile uint32_t*)lease.D().stat_host;   // an earlier launch's count (a hint)
+    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st, vr::crawl_grid(expect));
     // (on a failed launch the slot is still fenced: a kernel of it may be queued)
     rc = lease.release(st);
     if (e != hipSuccess) return hip_fail(e, "ray-march launch");

@@ -85,6 +85,7 @@ struct KView {
     uint32_t* defer;          // crawl deferral slot: [count, done, overflow, 0, records (kDeferRecWords each)...]
     uint32_t defer_cap;
     uint32_t crawl_rewalk;    // 1: deferred crawls are walked from the pixel's start (VR_KERNEL_TILE_REWALK)
+    uint32_t* defer_stat;     // host-mapped word: the crawl pass writes its record count there (grid sizing)
 };
 
 // Rays that start a cluster-skip crawl (see vr_march.hip crawl_steps) in the
@@ -105,9 +106,12 @@ constexpr uint32_t kDeferCap = 16384;
 constexpr uint32_t kDeferRecWords = 20;
 constexpr uint32_t kDeferWords = 4 + kDeferCap * kDeferRecWords;
 
-// Launch one render (defined in vr_march.hip): the tile pass and the crawl pass on `stream`.
+// Launch one render (defined in vr_march.hip): the tile pass and the crawl pass on
+// `stream`, the crawl pass with `crawl_wgs` workgroups (any number is correct).
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,
-                        hipStream_t stream);
+                        hipStream_t stream, uint32_t crawl_wgs);
+// Crawl-pass grid for a launch that expects about `records` deferred pixels.
+uint32_t crawl_grid(uint32_t records);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);
 
 }  // namespace vr

@@ -17,6 +17,8 @@
 // only on (hit origin, region, shadow algorithm), so the pixel is identical.
 #include "vr_device.h"
 
+#include <algorithm>
+
 // VR_DIAG (profiling builds only, profiles/wave_counts.py): wave-level execution
 // counters -- one atomic per wave per counted event, from the wave's first
 // active lane.  Never part of the library build.
@@ -891,7 +893,9 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
         // One exit per iteration (each extra exit of a divergent loop costs lane-mask
         // bookkeeping on every iteration): a lane that must leave computes the rest
         // of the iteration on stale values and leaves at its end, with the reason
-        enum : uint32_t { kGo = 0, kHit = 1, kLeft = 2, kOver = 3, kTail = 4 };   // kOver: past the budget
+        // kOver: past the budget; kCrawl (tile pass): a cluster skip with t = 0 -- a jump
+        // crawl, 10^4..10^6 iterations in the reference: the crawl pass walks the pixel
+        enum : uint32_t { kGo = 0, kHit = 1, kLeft = 2, kOver = 3, kTail = 4, kCrawl = 5 };
         uint32_t why = kGo, it = this->iters;
         VR_DIAG_COUNT(SHADOW ? 19 : 17);               // longest-axis walks
         for (;;) {
@@ -936,6 +940,11 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                 oL = oL + tMin * dL; oM = oM + tMin * dM; oS = oS + tMin * dS;
                 gL = f2i(floorf(oL)); gM = f2i(floorf(oM)); gS = f2i(floorf(oS));
                 if (ex == kGo && !grid_in_region(gL, gM, gS)) ex = kLeft;   // left the region: no tail
+                // t = 0: the ray stood on a cluster plane.  When EPSILON * d cannot move it
+                // off (the axis is still on the plane after the step) every further skip in
+                // this cluster is the same: a crawl, for the crawl pass.  A one-off walks on.
+                // (The t = 0 axis is M or S: |d_L| ~ 1, so EPSILON * d_L always moves L.)
+                if (!CRAWL && ex == kGo && tm0 == 0.0f && (oM == pM || oS == pS)) ex = kCrawl;
                 if constexpr (CRAWL) {
                     if (ex == kGo) {
                         if (this->same_f(oL, pL) && this->same_f(oM, pM) && this->same_f(oS, pS) && gL == qL &&
@@ -1048,7 +1057,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             jumping = stop != 3u;                    // jump on / start a jump; CONTINUE_VAL ends one
         }
         this->iters = it;
-        if (why == kOver) {
+        if (why == kOver || why == kCrawl) {   // (tile pass: shade hands the pixel to the crawl pass)
             aborted = true;
             return false;
         }
@@ -1397,6 +1406,10 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, ALGO == ALGO_ORIGINAL ? VR_
 
 // Crawl pass: the deferred pixels of this launch, one per lane, with the
 // exact crawl fast-forward; the last workgroup resets the slot for reuse.
+#ifndef VR_CRAWL_RPW
+#define VR_CRAWL_RPW 4
+#endif
+constexpr uint32_t kCrawlRpw = VR_CRAWL_RPW;
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     __shared__ uint32_t n_lds, ovf_lds;
@@ -1406,10 +1419,17 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     }
     __syncthreads();
     const uint32_t total = n_lds, overflow = ovf_lds;
+    // what this launch deferred, for the host's grid size of later launches (a hint only)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && v.defer_stat) *v.defer_stat = total + overflow;
     if (total == 0u && overflow == 0u) return;   // nothing deferred (the usual case): no reset needed
     const uint32_t n = min(total, v.defer_cap);
     unsigned long long bytes = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    // kCrawlRpw records per wave at a time (lanes 0 .. kCrawlRpw-1): each record is a long
+    // chain of dependent iterations, and the lanes of a wave take different paths through
+    // the walk, so fewer lanes per wave -- spread over more waves -- finish sooner
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, wlane = threadIdx.x & 63u;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t i = wave * kCrawlRpw + wlane; wlane < kCrawlRpw && i < n; i += nwaves * kCrawlRpw) {
         uint32_t* r = v.defer + 4 + (size_t)i * kDeferRecWords;
         uint32_t b;
         const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
@@ -1472,14 +1492,24 @@ __global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __rest
 // was deferred), both on `stream`.  (The crawl pass on a high-priority side stream,
 // fenced by events, measured slower on every config: C2 0.1148 -> 0.1224 ms per frame
 // with two in flight, 0.154 -> 0.184 alone; profiles/r03/ab_crawl_stream.txt.)
-hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream) {
+// The crawl pass's grid: kCrawlRpw records per wave, all of them at once (each record is
+// a latency-bound chain: C5 rpw 64 / 16 / 8 / 4 -> 0.93 / 0.82 / 0.80 / 0.76 ms per frame in
+// flight, profiles/r03/ab_crawl_rpw.txt), at least 64 workgroups.  The host sizes it from
+// the count an earlier launch of the device wrote to defer_stat: a launch that defers
+// nothing (C2-C4) keeps the small grid (1024 empty workgroups cost C2 0.6 %).
+uint32_t crawl_grid(uint32_t records) {
+    const uint32_t waves_per_wg = kTilesX * kTilesY;
+    const uint64_t waves = ((uint64_t)records * 5u / 4u + kCrawlRpw - 1u) / kCrawlRpw;
+    const uint64_t wgs = (waves + waves_per_wg - 1u) / waves_per_wg;
+    return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(wgs, 64u), 4096u);
+}
+
+hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream,
+                        uint32_t crawl_wgs) {
     dim3 grid((v.W + 8u * kTilesX - 1u) / (8u * kTilesX), (v.local_rows + 8u * kTilesY - 1u) / (8u * kTilesY));
     dim3 block(64u * kTilesX * kTilesY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-#ifndef VR_CRAWL_WGS
-#define VR_CRAWL_WGS 64
-#endif
-    const dim3 cgrid(VR_CRAWL_WGS);
+    const dim3 cgrid(crawl_wgs ? crawl_wgs : 64u);
 #define VR_LAUNCH(ST, AL, CT)                                                                     \
     do {                                                                                           \
         hipLaunchKernelGGL((march_kernel<ST, AL, CT>), grid, block, 0, stream, s, v);              \
