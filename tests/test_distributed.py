@@ -131,3 +131,25 @@ def test_band_gather_single_rank_is_the_frame():
     pipe.step(render)
     pipe.drain()
     assert len(got) == 2 and all(torch.equal(g, ref) for g in got)
+
+
+def test_fixed_tiling_eight_ranks_4k():
+    """BASELINE C5 as defined: ONE 3840x2160 frame over 8 ranks (bench.py --tiling fixed,
+    the default for C5): 8-row bands dealt round-robin, gathered over gloo to rank 0 and
+    assembled -- the frame comes back whole."""
+    from voxelraymarcher_amd.tiles import frame_resolution
+    world = 8
+    W, H = frame_resolution(3840, 2160, world, "fixed")
+    assert (W, H) == (3840, 2160)
+    assert frame_resolution(3840, 2160, world, "weak") != (3840, 2160)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, 8, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok, tmax = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert ok and tmax == world - 1

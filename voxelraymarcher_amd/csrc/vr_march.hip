@@ -1504,6 +1504,15 @@ uint32_t crawl_grid(uint32_t records) {
     return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(wgs, 64u), 4096u);
 }
 
+// VR_NO_CRAWL_PASS: a measurement-only build without the crawl pass (its cost on a
+// frame that defers nothing, C2: profiles/r03/ab_no_crawl_pass_C2.txt); wrong for any
+// frame that defers a pixel.
+#ifdef VR_NO_CRAWL_PASS
+constexpr bool kNoCrawlPass = true;
+#else
+constexpr bool kNoCrawlPass = false;
+#endif
+
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream,
                         uint32_t crawl_wgs) {
     dim3 grid((v.W + 8u * kTilesX - 1u) / (8u * kTilesX), (v.local_rows + 8u * kTilesY - 1u) / (8u * kTilesY));
@@ -1513,7 +1522,7 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
 #define VR_LAUNCH(ST, AL, CT)                                                                     \
     do {                                                                                           \
         hipLaunchKernelGGL((march_kernel<ST, AL, CT>), grid, block, 0, stream, s, v);              \
-        if (v.defer) hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, block, 0, stream, s, v); \
+        if (v.defer && !kNoCrawlPass) hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, block, 0, stream, s, v); \
     } while (0)
     if (store == STORE_VCS) {
         if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, false); }
