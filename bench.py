@@ -65,8 +65,10 @@ def parse():
     p.add_argument("--config", default="C2", choices=sorted(vr.CONFIGS))
     p.add_argument("--tiling", default="auto", choices=["auto", "weak", "fixed"])
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--frames-in-flight", type=int, default=2,
-                   help="band buffers/streams of the frame pipeline (1 = one frame at a time, for PMC passes)")
+    p.add_argument("--frames-in-flight", type=int, default=0,
+                   help="band buffers/streams of the frame pipeline (1 = one frame at a time, for PMC passes; "
+                        "default: 3 for C5, whose frames end in a latency-bound crawl pass, else 2 -- "
+                        "profiles/r03/frames_in_flight.txt)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="oracle threads (default: the CPUs this process may run on, at most OMP_NUM_THREADS)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -201,7 +203,8 @@ def main():
     stream = torch.cuda.current_stream()
     # N > 1: bands travel as the RGB8 framebuffer (writeColorToFramebuffer's format, 3 B per
     # pixel): rank 0 ends each frame with the RGB8 image
-    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=args.frames_in_flight, rgb8=world > 1)
+    depth = args.frames_in_flight or (3 if args.config == "C5" else 2)
+    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=depth, rgb8=world > 1)
 
     def render(buf):   # on the current stream (BandGather's slot stream in the loops)
         vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, rank, world, buf)
