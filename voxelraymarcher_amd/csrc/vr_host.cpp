@@ -435,6 +435,24 @@ int make_view(const vr_scene* s, const vr_camera* cam, const vr_lighting* lit, c
         v.Lr[i] = 1.0f / v.L[i];
         if (!(a >= 0x1p-64f && a <= 0x1p+20f)) v.L_fast = 0u;
     }
+    {
+        // the light's longest-axis frame, in the device's fp32 order (-ffp-contract=off)
+        const float ax = std::fabs(v.L[0]), ay = std::fabs(v.L[1]), az = std::fabs(v.L[2]);
+        const uint32_t order =
+            (ax > ay && ax > az) ? (ay > az ? 0u : 1u) : (ay > az ? (ax > az ? 2u : 3u) : (ax > ay ? 4u : 5u));
+        const float k = 1.0f / (order < 2u ? ax : (order < 4u ? ay : az));
+        uint32_t cls = 0;
+        bool unit = order == 5u && ax == ay && ay == az;
+        for (int i = 0; i < 3; ++i) {
+            v.Lw[i] = k * v.L[i];
+            cls |= (uint32_t)(v.Lw[i] > 0.0f) << (2 * i) | (uint32_t)(v.Lw[i] < 0.0f) << (2 * i + 1);
+            unit = unit && std::fabs(v.Lw[i]) == 1.0f;
+        }
+        v.L_order = order;
+        v.L_cls = cls;
+        v.L_unit = unit ? 1u : 0u;
+        v.L_eq = (v.L[0] == v.L[1] && v.L[1] == v.L[2]) ? 1u : 0u;
+    }
     v.scale_f = (float)scale;          // static_cast<float>(scale) (Ray.cuh:16)
     v.use_point_light = lit->use_point_light ? 1 : 0;
     v.use_shadows = lit->use_shadows ? 1 : 0;

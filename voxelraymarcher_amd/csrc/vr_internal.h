@@ -74,6 +74,13 @@ struct KView {
     // domain -- kernel arguments, so the shadow walks keep them in SGPRs
     float Lr[3];
     uint32_t L_fast;
+    // the light as a longest-axis walk sees it (Ray::convertRayToLongestAxisDirection,
+    // Ray.cuh:19-71): axis order 0..5 (L,M,S = xyz, xzy, yxz, yzx, zxy, zyx), direction
+    // k * L with k = 1 / |L_L| (xyz), its sign classes (bit 2a: > 0, bit 2a+1: < 0),
+    // L_unit = that direction is (+-1, +-1, +-1) exactly and the order is zyx (equal
+    // magnitudes), L_eq = L's three components are equal
+    float Lw[3];
+    uint32_t L_order, L_cls, L_unit, L_eq;
     float translation[3];
     float scale_f;
     int32_t use_point_light, use_shadows;

@@ -216,6 +216,13 @@ constexpr uint32_t kTilesX = VR_TILES_X, kTilesY = VR_TILES_Y;
 #ifndef VR_LONG_TAIL_GENERIC
 #define VR_LONG_TAIL_GENERIC false
 #endif
+// VR_LONG_TAIL_EQ: the original-DDA tail of a longest-axis shadow walk takes the
+// one-division loop when the light's components are equal (as the original
+// algorithm's shadow walks do).  Measured neutral on C3 (0.2722 vs 0.2736 ms alone,
+// profiles/r03/ab_la_signs_unit_C3.txt): off, the tail stays one loop.
+#ifndef VR_LONG_TAIL_EQ
+#define VR_LONG_TAIL_EQ 0
+#endif
 
 // The iteration count of a tile-pass walk that wrote a crawl record (see the deferral
 // in grid_original_rt): the pixel is the crawl pass's already.
@@ -840,13 +847,22 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
     // the original DDA from oo, Renderer.cuh:912-914, once for every order).
     template <int A>
     __device__ __forceinline__ static float ax3(f3 v) { return A == 0 ? v.x : (A == 1 ? v.y : v.z); }
-    template <bool SHADOW, int PL, int PM, int PS>
-    __device__ __forceinline__ bool walk_longest_vcs(f3& oo, f3 od, uint32_t reg, bool& tail, uint32_t& hcol,
-                                                     uint32_t& hcode) {
-        // Ray::convertRayToLongestAxisDirection (Ray.cuh:19-71)
-        const float odL = ax3<PL>(od), odM = ax3<PM>(od), odS = ax3<PS>(od);
-        const float k = 1.0f / fabsf(odL);
-        const float dL = k * odL, dM = k * odM, dS = k * odS;
+    // ds: the longest-axis direction k * d (Ray.cuh:19-71, made by the caller);
+    // cls: its sign classes, the same for every lane of the pass (an SGPR): bit 2a
+    // = ds_a > 0, bit 2a+1 = ds_a < 0 (a zero or NaN component is neither), so every
+    // direction-sign choice of the walk -- axisDiff[L], decimalToIntFunc, the jump's
+    // cluster planes, tNext's ceil/floor -- is a scalar select, not a per-lane mask.
+    // UNIT (shadow walks of a light whose ds is (+-1, +-1, +-1) exactly, e.g. the
+    // reference's normalize(1,1,1), Main.cu:28): every division by ds_a is exact
+    // negation or identity, so it is one multiply (x / +-1 == x * +-1 for every x).
+    template <bool SHADOW, bool UNIT, int PL, int PM, int PS>
+    __device__ __forceinline__ bool walk_longest_vcs(f3& oo, const f3 ds, const uint32_t cls, uint32_t reg,
+                                                     bool& tail, uint32_t& hcol, uint32_t& hcode) {
+        const float dL = ax3<PL>(ds), dM = ax3<PM>(ds), dS = ax3<PS>(ds);
+        auto dv = [](float n, float d) { return UNIT ? n * d : n / d; };
+        const bool posL = (cls >> (2 * PL)) & 1u, posM = (cls >> (2 * PM)) & 1u, posS = (cls >> (2 * PS)) & 1u;
+        const bool negL = (cls >> (2 * PL + 1)) & 1u, negM = (cls >> (2 * PM + 1)) & 1u;
+        const int32_t offL = posL ? 8 : 0, offM = posM ? 8 : 0, offS = posS ? 8 : 0;
         // walk frame <-> grid axes (x, y, z): constant indices, registers only
         auto xyz = [](auto l, auto m, auto s) {
             struct { decltype(l) c[3]; } r;
@@ -871,7 +887,8 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
         };
         float oL = ax3<PL>(oo), oM = ax3<PM>(oo), oS = ax3<PS>(oo);      // oldRay origin
         int32_t gL = f2i(oL), gM = f2i(oM), gS = f2i(oS);                 // gridValues
-        const int32_t aL = odL < 0.0f ? -1 : 1;                           // axisDiff[L]
+        // axisDiff[L] (d_L < 0 <=> ds_L < 0: k > 0, or k = inf with d = 0, or NaN)
+        const int32_t aL = negL ? -1 : 1;
         float rL, rM, rS;                                                 // ray origin
         {
             // x / (float)aL with aL = +-1 is exactly x * aL
@@ -879,7 +896,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             rL = oL + t * dL; rM = oM + t * dM; rS = oS + t * dS;
         }
         int32_t aM = f2i(rM) - gM, aS = f2i(rS) - gS;
-        const bool mid_floor = dM < 0.0f;                                 // decimalToIntFunc (:784)
+        const bool mid_floor = negM;                                      // decimalToIntFunc (:784)
         // (IEEE divisions: hoisted reciprocals (div_fast) measured slower here, C3
         // 0.385 -> 0.413 ms -- three more VGPRs live through the loop)
         const uint32_t moff = reg << 16;              // SGPR-base loads (see grid_original_rt)
@@ -915,7 +932,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                 const bool hasM = aM != 0, hasS = aS != 0;
                 bool sfirst = false;
                 if (hasM && hasS) {
-                    const float t1 = ((mid_floor ? floorf(oM) : ceilf(oM)) - oM) / dM;
+                    const float t1 = dv((mid_floor ? floorf(oM) : ceilf(oM)) - oM, dM);
                     const float sp = oS + dS * t1;
                     sfirst = f2i(floorf(sp)) - gS != 0;
                 }
@@ -927,11 +944,16 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             } else {
                 ++it;                                // tick()
                 ex = it > kBudget ? kOver : kGo;
-                // performVoxelSpaceJump's cluster skip (:707-725), integer planes from g
-                const int32_t nL = dL > 0.0f ? ((gL / 8) + 1) * 8 : (gL / 8) * 8;
-                const int32_t nM = dM > 0.0f ? ((gM / 8) + 1) * 8 : (gM / 8) * 8;
-                const int32_t nS = dS > 0.0f ? ((gS / 8) + 1) * 8 : (gS / 8) * 8;
-                const auto t = xyz(((float)nL - oL) / dL, ((float)nM - oM) / dM, ((float)nS - oS) / dS);
+                // performVoxelSpaceJump's cluster skip (:707-725), integer planes from g:
+                // d > 0 ? ((g / 8) + 1) * 8 : (g / 8) * 8.  (g / 8) * 8 is g & ~7 for g >= 0
+                // (a walk's cells never go below 0; the C division form for any wave
+                // holding a negative one)
+                int32_t bL = gL & ~7, bM = gM & ~7, bS = gS & ~7;
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64((gL | gM | gS) < 0) != 0, 0)) {
+                    bL = (gL / 8) * 8; bM = (gM / 8) * 8; bS = (gS / 8) * 8;
+                }
+                const int32_t nL = bL + offL, nM = bM + offM, nS = bS + offS;
+                const auto t = xyz(dv((float)nL - oL, dL), dv((float)nM - oM, dM), dv((float)nS - oS, dS));
                 const float tm0 = fminf(t.c[0], fminf(t.c[1], t.c[2]));
                 const float tMin = tm0 + kEps;
                 nj = t.c[0] == tMin ? 0u : (t.c[1] == tMin ? 1u : 2u);
@@ -1037,7 +1059,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             }
             if (jumping && stop == 3u) {
                 // landed in an existing cluster without a hit: CONTINUE_VAL (:740-750)
-                const float tNext = ((dL > 0.0f ? ceilf(oL) : floorf(oL)) - oL) / dL;
+                const float tNext = dv((posL ? ceilf(oL) : floorf(oL)) - oL, dL);
                 rL = oL + (tNext + kEps) * dL; rM = oM + (tNext + kEps) * dM; rS = oS + (tNext + kEps) * dS;
             }
             if (!jumping) {
@@ -1091,27 +1113,58 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
     }
     template <bool SHADOW>
     __device__ __forceinline__ bool grid_longest_vcs(f3& oo, f3 od, uint32_t reg, i3 cr, Hit& h) {
-        // the axis order of convertRayToLongestAxisDirection (Ray.cuh:19-71)
-        const float ax = fabsf(od.x), ay = fabsf(od.y), az = fabsf(od.z);
-        const uint32_t order = (ax > ay && ax > az) ? (ay > az ? 0u : 1u) : (ay > az ? (ax > az ? 2u : 3u) : (ax > ay ? 4u : 5u));
-        bool hit = false, tail = false, todo = true;
+        bool hit = false, tail = false;
         uint32_t hcol = 0, hcode = 0;
-        while (todo) {                                // one pass per order present in the wave
-            const uint32_t pat = __builtin_amdgcn_readfirstlane(order);
-            if (order == pat) {
-                todo = false;
-                switch (pat) {
-                    case 0: hit = walk_longest_vcs<SHADOW, 0, 1, 2>(oo, od, reg, tail, hcol, hcode); break;
-                    case 1: hit = walk_longest_vcs<SHADOW, 0, 2, 1>(oo, od, reg, tail, hcol, hcode); break;
-                    case 2: hit = walk_longest_vcs<SHADOW, 1, 0, 2>(oo, od, reg, tail, hcol, hcode); break;
-                    case 3: hit = walk_longest_vcs<SHADOW, 1, 2, 0>(oo, od, reg, tail, hcol, hcode); break;
-                    case 4: hit = walk_longest_vcs<SHADOW, 2, 0, 1>(oo, od, reg, tail, hcol, hcode); break;
-                    default: hit = walk_longest_vcs<SHADOW, 2, 1, 0>(oo, od, reg, tail, hcol, hcode); break;
+        if (SHADOW) {
+            // the light: its axis order, longest-axis direction and sign classes are
+            // made on the host (kernel arguments: SGPRs), one pass
+            const f3 ds = ld3(v.Lw);
+            if (v.L_unit) {
+                hit = walk_longest_vcs<SHADOW, true, 2, 1, 0>(oo, ds, v.L_cls, reg, tail, hcol, hcode);
+            } else {
+                switch (v.L_order) {
+                    case 0: hit = walk_longest_vcs<SHADOW, false, 0, 1, 2>(oo, ds, v.L_cls, reg, tail, hcol, hcode); break;
+                    case 1: hit = walk_longest_vcs<SHADOW, false, 0, 2, 1>(oo, ds, v.L_cls, reg, tail, hcol, hcode); break;
+                    case 2: hit = walk_longest_vcs<SHADOW, false, 1, 0, 2>(oo, ds, v.L_cls, reg, tail, hcol, hcode); break;
+                    case 3: hit = walk_longest_vcs<SHADOW, false, 1, 2, 0>(oo, ds, v.L_cls, reg, tail, hcol, hcode); break;
+                    case 4: hit = walk_longest_vcs<SHADOW, false, 2, 0, 1>(oo, ds, v.L_cls, reg, tail, hcol, hcode); break;
+                    default: hit = walk_longest_vcs<SHADOW, false, 2, 1, 0>(oo, ds, v.L_cls, reg, tail, hcol, hcode); break;
+                }
+            }
+        } else {
+            // the axis order of convertRayToLongestAxisDirection (Ray.cuh:19-71) and
+            // the longest-axis direction k * d, k = 1 / |d_L|
+            const float ax = fabsf(od.x), ay = fabsf(od.y), az = fabsf(od.z);
+            const uint32_t order =
+                (ax > ay && ax > az) ? (ay > az ? 0u : 1u) : (ay > az ? (ax > az ? 2u : 3u) : (ax > ay ? 4u : 5u));
+            const float k = 1.0f / (order < 2u ? ax : (order < 4u ? ay : az));
+            const f3 ds = scl(k, od);
+            const uint32_t cls = (uint32_t)(ds.x > 0.0f) | (uint32_t)(ds.x < 0.0f) << 1 | (uint32_t)(ds.y > 0.0f) << 2 |
+                                 (uint32_t)(ds.y < 0.0f) << 3 | (uint32_t)(ds.z > 0.0f) << 4 | (uint32_t)(ds.z < 0.0f) << 5;
+            const uint32_t key = order | cls << 3;
+            bool todo = true;
+            while (todo) {                            // one pass per (order, signs) present in the wave
+                const uint32_t pat = __builtin_amdgcn_readfirstlane(key);
+                if (key == pat) {
+                    todo = false;
+                    const uint32_t pc = pat >> 3;
+                    switch (pat & 7u) {
+                        case 0: hit = walk_longest_vcs<SHADOW, false, 0, 1, 2>(oo, ds, pc, reg, tail, hcol, hcode); break;
+                        case 1: hit = walk_longest_vcs<SHADOW, false, 0, 2, 1>(oo, ds, pc, reg, tail, hcol, hcode); break;
+                        case 2: hit = walk_longest_vcs<SHADOW, false, 1, 0, 2>(oo, ds, pc, reg, tail, hcol, hcode); break;
+                        case 3: hit = walk_longest_vcs<SHADOW, false, 1, 2, 0>(oo, ds, pc, reg, tail, hcol, hcode); break;
+                        case 4: hit = walk_longest_vcs<SHADOW, false, 2, 0, 1>(oo, ds, pc, reg, tail, hcol, hcode); break;
+                        default: hit = walk_longest_vcs<SHADOW, false, 2, 1, 0>(oo, ds, pc, reg, tail, hcol, hcode); break;
+                    }
                 }
             }
         }
         if (aborted) return false;
-        if (tail) return grid_original_rt(oo, od, reg, cr, h, SHADOW, false, nullptr, nullptr, VR_LONG_TAIL_GENERIC);
+        // the original-DDA tail; a shadow walk of an equal-component light takes the
+        // one-division loop (grid_original's EQ)
+        if (tail)
+            return grid_original_rt(oo, od, reg, cr, h, SHADOW, SHADOW && VR_LONG_TAIL_EQ && v.L_eq, nullptr, nullptr,
+                                    VR_LONG_TAIL_GENERIC);
         if (!SHADOW && hit) {
             const float one = (hcode & 4u) ? 1.0f : -1.0f;
             const uint32_t a = hcode & 3u;
