@@ -1,4 +1,7 @@
+# A/B call (GPU box): parity of the first library under test, then ab_inflight over all of them.
+#   bash profiles/r03/cmd_ab.sh <out> <config> <steps> lib1 lib2 ...
 set -o pipefail
-O=gpurun_out/ab1; mkdir -p $O
-VR_LIBRARY=$PWD/voxelraymarcher_amd/ab/libvr_la1.so timeout -k 10 300 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests_la1.log 2>&1 &&
-timeout -k 10 400 python profiles/ab_inflight.py C3 200 voxelraymarcher_amd/ab/libvr_base.so voxelraymarcher_amd/ab/libvr_la1.so voxelraymarcher_amd/ab/libvr_la1noeq.so --rounds 2 > $O/ab_C3.txt 2>&1
+O=$1; C=$2; K=$3; shift 3
+mkdir -p $O
+VR_LIBRARY=$PWD/$1 timeout -k 10 300 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.log 2>&1 &&
+timeout -k 10 500 python profiles/ab_inflight.py $C $K "$@" --rounds 2 > $O/ab_$C.txt 2>&1

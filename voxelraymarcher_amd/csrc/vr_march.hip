@@ -1577,6 +1577,13 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
         hipLaunchKernelGGL((march_kernel<ST, AL, CT>), grid, block, 0, stream, s, v);              \
         if (v.defer && !kNoCrawlPass) hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, block, 0, stream, s, v); \
     } while (0)
+#ifdef VR_ISA_ONLY
+    // ISA-inspection builds (csrc/Makefile isa1, profiles/loop_isa.py): one kernel pair
+    // only, e.g. -DVR_ISA_ONLY=ALGO_LONGEST for the VCS longest-axis tile pass; never a library
+    (void)algo; (void)count; (void)store;
+    VR_LAUNCH(STORE_VCS, VR_ISA_ONLY, false);
+    return hipGetLastError();
+#endif
     if (store == STORE_VCS) {
         if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, false); }
         else { if (count) VR_LAUNCH(STORE_VCS, ALGO_LONGEST, true); else VR_LAUNCH(STORE_VCS, ALGO_LONGEST, false); }
