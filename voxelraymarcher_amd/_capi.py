@@ -49,11 +49,13 @@ class VrSynthParams(ctypes.Structure):
 
 
 VR_KERNEL_AUTO, VR_KERNEL_TILE, VR_KERNEL_TILE_REWALK = 0, 1, 3
+VR_SCHEDULE_AUTO, VR_SCHEDULE_GRID, VR_SCHEDULE_HEAVIEST_FIRST = 0, 1, 2
 
 
 class VrRenderOpts(ctypes.Structure):
     _fields_ = [("kernel", c_uint32), ("row_begin", c_uint32), ("row_end", c_uint32), ("band_rows", c_uint32),
-                ("rank", c_uint32), ("nranks", c_uint32), ("bytes_dev", c_void_p), ("defer_cap", c_uint32)]
+                ("rank", c_uint32), ("nranks", c_uint32), ("bytes_dev", c_void_p), ("defer_cap", c_uint32),
+                ("schedule", c_uint32)]
 
 
 class VrError(RuntimeError):
@@ -125,6 +127,6 @@ def f3(v) -> ctypes.Array:
     return (c_float * 3)(*[float(x) for x in v])
 
 
-__all__ = ["lib", "check", "VrCamera", "VrLighting", "VrRenderOpts", "VR_KERNEL_AUTO", "VR_KERNEL_TILE", "VR_KERNEL_TILE_REWALK", "VrSceneInfo", "VrSynthParams", "VrError", "SIGNATURES",
+__all__ = ["lib", "check", "VrCamera", "VrLighting", "VrRenderOpts", "VR_KERNEL_AUTO", "VR_KERNEL_TILE", "VR_KERNEL_TILE_REWALK", "VR_SCHEDULE_AUTO", "VR_SCHEDULE_GRID", "VR_SCHEDULE_HEAVIEST_FIRST", "VrSceneInfo", "VrSynthParams", "VrError", "SIGNATURES",
            "VR_STORE_VCS", "VR_STORE_HASHTABLE", "VR_ALGO_LONGESTAXIS", "VR_ALGO_ORIGINAL", "f3", "LIB_PATH",
            "c_uint8"]

@@ -484,6 +484,18 @@ struct SlotRing {
         uint32_t next = 0;
         uint32_t* stat_host = nullptr;     // host-mapped: the last crawl pass's record count
         uint32_t* stat_dev = nullptr;
+        // per slot: the tile pass's work order (heaviest tile groups first) made from the
+        // costs of the slot's last launch that recorded them, for a grid of gx x gy
+        struct Order {
+            uint32_t* cost = nullptr;      // kWavesPerTileGroup words per tile group
+            uint32_t* order = nullptr;     // one word per tile group
+            uint32_t cap = 0, gx = 0, gy = 0, age = 0;
+            bool valid = false;
+        };
+        std::vector<Order> ord;
+        bool any = false;                  // the device's previous launch: its stream and slot
+        hipStream_t last_stream = nullptr;
+        uint32_t last_idx = 0;
     } dev[64];
     SlotRing(const char* n, size_t w, uint32_t s) : name(n), words(w), nslots(s) {}
 };
@@ -522,6 +534,7 @@ int ring_init(SlotRing& r, SlotRing::Dev& D) {
     if (e != hipSuccess) return undo(e, "hipHostMalloc(crawl statistics)");
     D.ev = std::move(ev);
     D.used.assign(r.nslots, false);
+    D.ord.assign(r.nslots, SlotRing::Dev::Order{});
     D.stat_host = (uint32_t*)h;
     D.stat_dev = (uint32_t*)hd;
     D.base = (uint32_t*)q;
@@ -565,7 +578,26 @@ struct SlotLease {
     }
 };
 
-int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void* stream) {
+// Heaviest-first work order: remade every VR_ORDER_REFRESH (16) launches of
+// a slot (16 slots: about one order build per 16 launches of a device).  VR_ORDER=0 turns
+// it off.
+uint32_t order_refresh() {
+    static const uint32_t r = [] {
+        const char* e = std::getenv("VR_ORDER_REFRESH");
+        const long v = e ? std::strtol(e, nullptr, 10) : 16;
+        return (uint32_t)(v >= 1 ? v : 16);
+    }();
+    return r;
+}
+bool order_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("VR_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, vr::KView& v, void* stream) {
     if (algo != VR_ALGO_ORIGINAL && algo != VR_ALGO_LONGESTAXIS) return fail(VR_E_INVALID, "unknown algorithm");
     if (kernel != VR_KERNEL_AUTO && kernel != VR_KERNEL_TILE && kernel != VR_KERNEL_TILE_REWALK)
         return fail(VR_E_INVALID, "unknown kernel (2, the persistent kernel, was retired)");
@@ -582,7 +614,69 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, vr::KView& v, void*
     v.defer_cap = (v.defer_cap && v.defer_cap < vr::kDeferCap) ? v.defer_cap : vr::kDeferCap;
     v.defer_stat = lease.D().stat_dev;
     const uint32_t expect = *(volatile uint32_t*)lease.D().stat_host;   // an earlier launch's count (a hint)
+    // The work order: this slot's order if it was made for this grid, remade (from this
+    // launch's costs, after its passes) when missing or every order_refresh() uses of the slot.
+    // It only permutes the tile groups; a view of the same grid size that it was not made
+    // for renders the same pixels, just in a worse order.
+    uint32_t gx = 0, gy = 0;
+    vr::march_grid(v, gx, gy);
+    const uint32_t n = gx * gy;
+    SlotRing::Dev& D = lease.D();
+    SlotRing::Dev::Order& O = D.ord[lease.idx];
+    bool remake = false;
+    bool heavy = schedule == VR_SCHEDULE_HEAVIEST_FIRST;
+    if (schedule == VR_SCHEDULE_AUTO)       // (the lock orders launches: "previous" is well defined)
+        heavy = !D.any || D.last_stream == st || hipEventQuery(D.ev[D.last_idx]) == hipSuccess;
+    D.any = true;
+    D.last_stream = st;
+    D.last_idx = lease.idx;
+    if (heavy && order_enabled() && n != 0) {
+        if (n > O.cap) {
+            // grow (the slot's previous launch is fenced on this stream; free waits for it)
+            hipError_t e = hipStreamSynchronize(st);
+            if (e == hipSuccess && O.cost) e = hipFree(O.cost);
+            if (e == hipSuccess && O.order) e = hipFree(O.order);
+            O = SlotRing::Dev::Order{};
+            if (e == hipSuccess) e = hipMalloc((void**)&O.cost, sizeof(uint32_t) * vr::kWavesPerTileGroup * (size_t)n);
+            if (e == hipSuccess) e = hipMalloc((void**)&O.order, sizeof(uint32_t) * (size_t)n);
+            if (e != hipSuccess) {
+                if (O.cost) (void)hipFree(O.cost);
+                if (O.order) (void)hipFree(O.order);
+                O = SlotRing::Dev::Order{};
+                return hip_fail(e, "work order buffers");
+            }
+            O.cap = n;
+        }
+        const bool match = O.valid && O.gx == gx && O.gy == gy;
+        v.order = match ? O.order : nullptr;
+        remake = !match || ++O.age >= order_refresh();
+        v.cost = remake ? O.cost : nullptr;
+    }
     hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st, vr::crawl_grid(expect));
+    if (e == hipSuccess && remake) {
+        // (on a side stream instead -- one more stream than the box's 4 hardware queues
+        // serialised the two render streams: C2 0.1124 -> 0.1277 ms per frame in flight,
+        // profiles/r03/ab_order_C2_C3.txt)
+        e = vr::launch_order(O.cost, n, gx, O.order, st);
+        if (std::getenv("VR_ORDER_CHECK")) {
+            std::vector<uint32_t> h(n), c(2 * (size_t)n);
+            (void)hipDeviceSynchronize();
+            (void)hipMemcpy(h.data(), O.order, 4 * (size_t)n, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(c.data(), O.cost, 8 * (size_t)n, hipMemcpyDeviceToHost);
+            std::vector<int> seen(n, 0);
+            int bad = 0;
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t t = (h[i] >> 16) * gx + (h[i] & 0xFFFFu);
+                if ((h[i] & 0xFFFFu) >= gx || t >= n || seen[t]++) ++bad;
+            }
+            fprintf(stderr, "[order] slot %u grid %ux%u n %u bad %d first %08x %08x cost0 %u %u\n", lease.idx, gx, gy, n,
+                    bad, h[0], n > 1 ? h[1] : 0u, c[0], c[1]);
+        }
+        O.valid = e == hipSuccess;
+        O.gx = gx;
+        O.gy = gy;
+        O.age = 0;
+    }
     // (on a failed launch the slot is still fenced: a kernel of it may be queued)
     rc = lease.release(st);
     if (e != hipSuccess) return hip_fail(e, "ray-march launch");
@@ -893,13 +987,14 @@ int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr
     v.out = out_dev;
     v.bytes = (unsigned long long*)opts->bytes_dev;
     v.defer_cap = opts->defer_cap;
-    return launch(s, algo, opts->kernel, v, stream);
+    if (opts->schedule > VR_SCHEDULE_HEAVIEST_FIRST) return fail(VR_E_INVALID, "unknown schedule");
+    return launch(s, algo, opts->kernel, opts->schedule, v, stream);
 }
 
 int vr_render(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit, const float translation[3],
               uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin, uint32_t row_end, uint32_t* out_dev,
               void* stream) {
-    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, nullptr, 0};
+    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, nullptr, 0, VR_SCHEDULE_AUTO};
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
@@ -914,7 +1009,7 @@ int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t band_rows,
                     uint32_t rank, uint32_t nranks, uint32_t* out_dev, void* stream) {
     if (!band_rows) return fail(VR_E_INVALID, "band_rows must be > 0");
-    vr_render_opts o{VR_KERNEL_AUTO, 0, height, band_rows, rank, nranks, nullptr, 0};
+    vr_render_opts o{VR_KERNEL_AUTO, 0, height, band_rows, rank, nranks, nullptr, 0, VR_SCHEDULE_AUTO};
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
@@ -922,7 +1017,7 @@ int vr_render_count(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin,
                     uint32_t row_end, uint32_t* out_dev, uint64_t* bytes_dev, void* stream) {
     if (!bytes_dev) return fail(VR_E_INVALID, "bytes_dev is NULL");
-    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, bytes_dev, 0};
+    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, bytes_dev, 0, VR_SCHEDULE_AUTO};
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 

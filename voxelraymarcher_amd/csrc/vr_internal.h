@@ -93,6 +93,13 @@ struct KView {
     uint32_t defer_cap;
     uint32_t crawl_rewalk;    // 1: deferred crawls are walked from the pixel's start (VR_KERNEL_TILE_REWALK)
     uint32_t* defer_stat;     // host-mapped word: the crawl pass writes its record count there (grid sizing)
+    // Tile-pass work order ("Heaviest tiles first"): workgroup i of the grid
+    // renders tile order[i] = (tile row << 16 | tile column) -- a permutation of the grid
+    // made from an earlier launch's costs -- or, when null, tile i in grid order.  cost
+    // (or null): each wave writes its walk length (the max over its lanes of the pixel's
+    // loop iterations) to cost[tile * kWavesPerTileGroup + wave], tile = row * columns + column.
+    const uint32_t* order;
+    uint32_t* cost;
 };
 
 // Rays that start a cluster-skip crawl (see vr_march.hip crawl_steps) in the
@@ -120,5 +127,11 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
 // Crawl-pass grid for a launch that expects about `records` deferred pixels.
 uint32_t crawl_grid(uint32_t records);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);
+// The tile pass's grid for a view (columns, rows of workgroups) and its waves per workgroup.
+void march_grid(const KView& v, uint32_t& columns, uint32_t& rows);
+constexpr uint32_t kWavesPerTileGroup = 2;
+// Heaviest-first work order of a grid of `columns` x `n / columns` workgroups from the
+// costs a launch wrote (KView::cost): one workgroup, a counting sort by cost.
+hipError_t launch_order(const uint32_t* cost, uint32_t n, uint32_t columns, uint32_t* order, hipStream_t stream);
 
 }  // namespace vr

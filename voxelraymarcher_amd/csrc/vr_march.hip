@@ -228,6 +228,19 @@ constexpr uint32_t kTilesX = VR_TILES_X, kTilesY = VR_TILES_Y;
 // in grid_original_rt): the pixel is the crawl pass's already.
 constexpr uint32_t kDeferredIters = 0xFFFFFFFFu;
 
+// The tile group (column, row of kTilesX x kTilesY tiles) this tile-pass workgroup
+// renders: the work order's entry (heaviest first, KView::order), or its grid position
+// (a uniform load: SGPRs).
+__device__ __forceinline__ void tile_group(const KView& v, uint32_t& bx, uint32_t& by) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    if (v.order) {
+        const uint32_t t = v.order[blockIdx.y * gridDim.x + blockIdx.x];
+        bx = t & 0xFFFFu;
+        by = t >> 16;
+    }
+}
+
 // CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
 // crawling ray reserves an entry in the launch's deferral list and unwinds.
 // kExact (the crawl pass): every walk runs to its end here, and a loop round that
@@ -550,9 +563,13 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                         if (idx < v.defer_cap) {
                             // (the tile pass writes this pixel as 0; the crawl pass,
                             // which runs after it, overwrites it and counts its bytes)
+                            // (the pixel again from the workgroup's tile group: not kept live
+                            // through the walk)
                             const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-                            const uint32_t px_ = (blockIdx.x * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
-                            const uint32_t pl_ = (blockIdx.y * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
+                            uint32_t tbx, tby;
+                            tile_group(v, tbx, tby);
+                            const uint32_t px_ = (tbx * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
+                            const uint32_t pl_ = (tby * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
                             uint32_t* r = v.defer + 4 + (size_t)idx * kDeferRecWords;
                             r[0] = (pl_ << 16) | px_;
                             r[1] = (SHADOW ? 1u : 0u) | this->ctx;
@@ -1379,7 +1396,7 @@ __device__ __forceinline__ uint32_t defer_rewalk(const KView& v, uint32_t x, uin
 // the oracle.
 template <int STORE, int ALGO, bool COUNT, bool CRAWL>
 __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint32_t x, uint32_t l,
-                                          uint32_t& bytes) {
+                                          uint32_t& bytes, uint32_t* iters = nullptr) {
     uint32_t col = 0;
     bytes = 0;
     f3 ro, rd;
@@ -1387,6 +1404,7 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
         Walker<STORE, COUNT, CRAWL> w(s, v);
         Hit h;
         if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
+        if (iters) *iters = w.iters;              // the walk's length (the work order's cost)
         bytes = w.bytes + 4u;                     // + the pixel write
         if (w.aborted) {
             col = 0;
@@ -1445,16 +1463,55 @@ __device__ __forceinline__ void add_bytes(const KView& v, uint32_t lane, unsigne
 #ifndef VR_LONG_WAVES
 #define VR_LONG_WAVES 6
 #endif
+static_assert(kTilesX * kTilesY == kWavesPerTileGroup, "cost layout (vr_internal.h)");
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(64 * kTilesX * kTilesY, ALGO == ALGO_ORIGINAL ? VR_ORIG_WAVES : VR_LONG_WAVES) void march_kernel(KScene s, KView v) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t x = (blockIdx.x * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
-    const uint32_t l = (blockIdx.y * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
-    uint32_t bytes = 0;
+    uint32_t bx, by;
+    tile_group(v, bx, by);
+    const uint32_t x = (bx * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
+    const uint32_t l = (by * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
+    uint32_t bytes = 0, iters = 0;
     if (x < v.W && l < v.local_rows) {
-        v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes);
+        v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes, v.cost ? &iters : nullptr);
     }
     if (COUNT) add_bytes(v, lane, bytes);
+    if (v.cost) {                                  // the wave's walk length, for the next work order
+        for (int off = 32; off > 0; off >>= 1) iters = max(iters, (uint32_t)__shfl_xor((int)iters, off, 64));
+        if (lane == 0) v.cost[(by * gridDim.x + bx) * kWavesPerTileGroup + wave] = iters;
+    }
+}
+
+// Heaviest tiles first: a counting sort of the tile groups by the cost an earlier
+// launch recorded (the slower of a workgroup's waves; classes of 4 loop iterations,
+// class 0 the heaviest, >= 508), in one workgroup with LDS counters.  The order within
+// a class is whatever the atomics make it: any permutation renders the same pixels.
+// (A stable sort -- grid order within a class, one ballot per class present per 64
+// groups -- took ~4x longer and gained nothing, profiles/r03/ab_order_C2_C3.txt.)
+constexpr uint32_t kOrderClasses = 128;
+__global__ __launch_bounds__(1024) void order_kernel(const uint32_t* __restrict__ cost, uint32_t n, uint32_t columns,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t cnt[kOrderClasses];
+    if (threadIdx.x < kOrderClasses) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    auto cls = [&](uint32_t i) {
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kWavesPerTileGroup; ++w) c = max(c, cost[i * kWavesPerTileGroup + w]);
+        return kOrderClasses - 1u - min(kOrderClasses - 1u, c >> 2);
+    };
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&cnt[cls(i)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {                        // exclusive prefix sum
+        uint32_t run = 0;
+        for (uint32_t k = 0; k < kOrderClasses; ++k) {
+            const uint32_t c = cnt[k];
+            cnt[k] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&cnt[cls(i)], 1u)] = (i / columns) << 16 | (i % columns);
 }
 
 // Crawl pass: the deferred pixels of this launch, one per lane, with the
@@ -1566,9 +1623,22 @@ constexpr bool kNoCrawlPass = true;
 constexpr bool kNoCrawlPass = false;
 #endif
 
+void march_grid(const KView& v, uint32_t& columns, uint32_t& rows) {
+    columns = (v.W + 8u * kTilesX - 1u) / (8u * kTilesX);
+    rows = (v.local_rows + 8u * kTilesY - 1u) / (8u * kTilesY);
+}
+
+hipError_t launch_order(const uint32_t* cost, uint32_t n, uint32_t columns, uint32_t* order, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, stream, cost, n, columns, order);
+    return hipGetLastError();
+}
+
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream,
                         uint32_t crawl_wgs) {
-    dim3 grid((v.W + 8u * kTilesX - 1u) / (8u * kTilesX), (v.local_rows + 8u * kTilesY - 1u) / (8u * kTilesY));
+    uint32_t gx, gy;
+    march_grid(v, gx, gy);
+    dim3 grid(gx, gy);
     dim3 block(64u * kTilesX * kTilesY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     const dim3 cgrid(crawl_wgs ? crawl_wgs : 64u);

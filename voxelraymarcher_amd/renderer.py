@@ -262,13 +262,23 @@ class Kernel(enum.IntEnum):
     TILE_REWALK = _capi.VR_KERNEL_TILE_REWALK
 
 
+class Schedule(enum.IntEnum):
+    """vr_schedule: the tile pass's work order (identical pixels).  AUTO: heaviest tile
+    groups first when the device's previous launch was on the same stream or has finished
+    (a lone frame's latency), grid order while another stream's launch runs (frames in flight)."""
+    AUTO = _capi.VR_SCHEDULE_AUTO
+    GRID = _capi.VR_SCHEDULE_GRID
+    HEAVIEST_FIRST = _capi.VR_SCHEDULE_HEAVIEST_FIRST
+
+
 def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
               info: VoxelSceneInfo, width: int, height: int, out: torch.Tensor, row_begin: int = 0,
               row_end: int | None = None, band_rows: int = 0, rank: int = 0, nranks: int = 1,
               counter: torch.Tensor | None = None, kernel: Kernel = Kernel.AUTO, stream=None,
-              defer_cap: int = 0) -> torch.Tensor:
+              defer_cap: int = 0, schedule: Schedule = Schedule.AUTO) -> torch.Tensor:
     """vr_render_ex: rows [row_begin,row_end), bands of band_rows (0 = one band) dealt to nranks ranks.
-    defer_cap: capacity of the crawl pass's deferral list (0 = default; small values force its overflow path)."""
+    defer_cap: capacity of the crawl pass's deferral list (0 = default; small values force its overflow path).
+    schedule: the tile pass's work order (Schedule)."""
     row_end = height if row_end is None else row_end
     rows = row_end - row_begin
     words = band_buffer_words(width, rows, band_rows or max(1, rows), nranks)
@@ -276,7 +286,8 @@ def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, 
     if counter is not None and (not counter.is_cuda or counter.dtype != torch.int64):
         raise TypeError("counter must be a CUDA int64 tensor")
     opts = _capi.VrRenderOpts(int(kernel), int(row_begin), int(row_end), int(band_rows), int(rank), int(nranks),
-                              c_void_p(counter.data_ptr()) if counter is not None else None, int(defer_cap))
+                              c_void_p(counter.data_ptr()) if counter is not None else None, int(defer_cap),
+                              int(schedule))
     check(lib().vr_render_ex(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
                              f3(info.translation), int(info.scale), int(width), int(height), ctypes.byref(opts),
                              c_void_p(out.data_ptr()), _stream_ptr(stream)), "vr_render_ex")
