@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Profiling driver: render one BASELINE config `--iters` times (kernel only,
-inputs resident), printing the HIP-event average per launch.  Run under
-rocprofv3 by profiles/r03/profile_round.sh."""
+inputs resident), one launch after another on one stream, printing the HIP-event
+average per launch.  `--warmup` untimed launches come first: they give every
+launch slot its heaviest-first work order (include/vr.h vr_schedule; the AUTO
+schedule of serialised launches), so the timed launches run as bench.py's
+kernel_ms launches do.  Run under rocprofv3 by profiles/r03/profile_round.sh;
+profiles/trace_avg.py averages the timed (last --iters) dispatches of the trace."""
 import argparse
 import os
 import sys
@@ -15,6 +19,7 @@ import voxelraymarcher_amd as vr  # noqa: E402
 p = argparse.ArgumentParser()
 p.add_argument("--config", default="C2")
 p.add_argument("--iters", type=int, default=20)
+p.add_argument("--warmup", type=int, default=40)
 p.add_argument("--no-shadows", action="store_true")
 p.add_argument("--algo", choices=["original", "longestaxis"], default=None)
 p.add_argument("--store", choices=["vcs", "hashtable"], default=None)
@@ -32,7 +37,8 @@ lit = vr.setup_constant_values(use_shadows=not a.no_shadows)
 info = vr.VoxelSceneInfo((0, 0, 0), cfg.scale)
 out = torch.empty(W * H, dtype=torch.int32, device="cuda")
 s = torch.cuda.current_stream()
-vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, kernel=kern)
+for _ in range(1 + a.warmup):
+    vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, kernel=kern)
 torch.cuda.synchronize()
 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
 for e0, e1 in ev:

@@ -16,6 +16,8 @@ for CFG in "$@"; do
   DRV="python3 profiles/profile_kernel.py --config $CFG --iters 20"
   run() { timeout -s KILL 120 "$@" >> "$D/log.txt" 2>&1; local rc=$?; if [ $rc -ne 0 ]; then echo "step failed rc=$rc: $*"; exit $rc; fi; }
   run rocprofv3 --kernel-trace --stats -f csv -d "$D/trace" -o run -- $DRV
+  # the timed (last 20) launches: heaviest-first order in every slot after the warmup
+  python3 profiles/trace_avg.py "$D/trace/run_kernel_trace.csv" 20 > "$D/kernel_timed.txt" || exit 1
   run rocprofv3 --pmc FETCH_SIZE --kernel-trace -f csv -d "$D/pmc_fetch" -o run -- $DRV
   run rocprofv3 --pmc WRITE_SIZE --kernel-trace -f csv -d "$D/pmc_write" -o run -- $DRV
   run rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD --kernel-trace -f csv -d "$D/pmc_sq" -o run -- $DRV
