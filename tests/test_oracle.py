@@ -329,3 +329,34 @@ def test_never_ending_walks():
     sc = oracle.Scene(np.array([[100, 100, 100]], np.int32), np.array([5], np.uint32), 0)
     img, nbytes = sc.render(1, cam, oracle.lighting(), 4, 4, 1)
     assert not img.any() and nbytes == 64
+
+
+@pytest.mark.parametrize("seed", list(range(1000, 1012)))
+def test_fuzz_cases_python_restatement(seed):
+    """The GPU fuzz cases (tests/fuzz_cases.py: random scenes, cameras, scales,
+    translations, light blocks): the oracle and the independent Python restatement
+    agree on 24 sampled pixels per store x algorithm."""
+    from tests.fuzz_cases import make_case
+    c = make_case(seed)
+    cam = oracle.camera(c.eye, c.look_at, c.up, c.fov, c.aspect)
+    plit = pyref.Lighting(c.shadows, c.point, c.light_pos)
+    if c.light_dir is not None:
+        plit.L = pyref.V(*c.light_dir).unit()                 # Main.cu:28 makeUnitVector
+    plit.LC = pyref.V(*c.light_color)
+    lit = oracle.lighting(use_shadows=c.shadows, use_point_light=c.point, light_position=c.light_pos)
+    for i in range(3):
+        lit.light_dir[i] = float(plit.L.x[i])
+        lit.light_color[i] = float(plit.LC.x[i])
+    rng = np.random.default_rng(seed)
+    px = rng.integers(0, c.W, 24).astype(np.uint32)
+    py = rng.integers(0, c.H, 24).astype(np.uint32)
+    pc = _pyref_camera(cam)
+    for store in (oracle.STORE_VCS, oracle.STORE_HASHTABLE):
+        sc = oracle.Scene(c.xyz, c.rgb, store)
+        ps = pyref.Scene(c.xyz, c.rgb, store)
+        for algo in (oracle.ALGO_ORIGINAL, oracle.ALGO_LONGESTAXIS):
+            got, _ = sc.render_pixels(algo, cam, lit, c.W, c.H, c.scale, px, py, translation=c.translation)
+            for i in range(len(px)):
+                want = pyref.render_pixel(ps, plit, pc, c.W, c.H, int(px[i]), int(py[i]), c.scale,
+                                          algo == oracle.ALGO_LONGESTAXIS, translation=c.translation)
+                assert int(got[i]) == want, (seed, store, algo, int(px[i]), int(py[i]), hex(int(got[i])), hex(want))
