@@ -159,14 +159,17 @@ static int vrec_cmp(const void* a, const void* b) {
 }
 
 /* Deterministic stand-in for Random::getRandomInt (Random.cuh:14-18); any
- * valid cuckoo placement yields identical lookups. */
+ * valid cuckoo placement yields identical lookup VALUES, but the
+ * bytes a lookup reads depend on the table a key sits in (4 more for table 2),
+ * so the stand-in is the product builder's (vr_host.cpp cuckoo_build): the same
+ * LCG, seeded from the region's key count and first key. */
 static uint32_t lcg_next(uint64_t* s) {
     *s = *s * 6364136223846793005ull + 1442695040888963407ull;
     return (uint32_t)(*s >> 33);
 }
 
 /* CuckooHashTable.cuh:20-49 + createCuckooHashTable :97-178 */
-static int cuckoo_build(or_cuckoo* t, const kv* e, uint32_t n, uint64_t seed) {
+static int cuckoo_build(or_cuckoo* t, const kv* e, uint32_t n) {
     t->M = (uint32_t)((double)n * 1.25);            /* :23 numElements * 1.25 */
     t->offset = 0; t->prime = PRIME_TABLE[0];
     t->k1 = (uint32_t*)malloc(sizeof(uint32_t) * t->M);
@@ -174,7 +177,7 @@ static int cuckoo_build(or_cuckoo* t, const kv* e, uint32_t n, uint64_t seed) {
     t->k2 = (uint32_t*)malloc(sizeof(uint32_t) * t->M);
     t->v2 = (uint32_t*)calloc(t->M, sizeof(uint32_t));
     if (!t->k1 || !t->v1 || !t->k2 || !t->v2) return -1;
-    uint64_t rng = seed;
+    uint64_t rng = 0x9E3779B97F4A7C15ull ^ (uint64_t)n ^ ((uint64_t)e[0].key << 20);
     for (int attempt = 0; attempt < 4096; ++attempt) {
         for (uint32_t i = 0; i < t->M; ++i) { t->k1[i] = EMPTY_VAL; t->k2[i] = EMPTY_VAL; t->v1[i] = 0; t->v2[i] = 0; }
         int rehash = 0;
@@ -296,7 +299,7 @@ int or_scene_build(int store, const int32_t* xyz, const uint32_t* rgb, size_t n,
             size_t j = i;
             while (j < m && recs[j].region == recs[i].region) ++j;
             for (size_t k = i; k < j; ++k) { tmp[k - i].key = recs[k].key; tmp[k - i].val = recs[k].val; }
-            if (cuckoo_build(&s->ht[r], tmp, (uint32_t)(j - i), 0x9E3779B97F4A7C15ull ^ r) != 0) rc_ok = -3;
+            if (cuckoo_build(&s->ht[r], tmp, (uint32_t)(j - i)) != 0) rc_ok = -3;
             ++r; i = j;
         }
         free(tmp);
