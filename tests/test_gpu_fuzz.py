@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 vr = pytest.importorskip("voxelraymarcher_amd")
 
-SEEDS = list(range(1000, 1048))
+SEEDS = list(range(1000, 1200))
 
 
 @pytest.mark.parametrize("seed", SEEDS)
