@@ -3,7 +3,7 @@
 algorithm, the GPU frame's pixels and algorithmic bytes against the oracle's; on a
 byte mismatch, the rows whose byte counts differ (one counted GPU launch per row)
 with the oracle's per-pixel bytes of those rows.
-  python profiles/fuzz_bytes_probe.py [first_seed] [n_seeds]"""
+  python profiles/fuzz_bytes_probe.py [first_seed] [n_seeds]     (seeds >= 5000: make_wide_case)"""
 import json
 import os
 import sys
@@ -16,13 +16,13 @@ sys.path.insert(0, ROOT)
 
 import oracle  # noqa: E402
 import voxelraymarcher_amd as vr  # noqa: E402
-from tests.fuzz_cases import make_case  # noqa: E402
+from tests.fuzz_cases import make_case, make_wide_case  # noqa: E402
 from tests.helpers import gpu_render, oracle_camera_from, oracle_lighting_from  # noqa: E402
 
 first = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 48
 for seed in range(first, first + n):
-    c = make_case(seed)
+    c = make_wide_case(seed) if seed >= 5000 else make_case(seed)
     cam = vr.Camera(c.eye, c.look_at, c.up, c.fov, c.aspect)
     lit = vr.setup_constant_values(use_shadows=c.shadows, use_point_light=c.point, light_position=c.light_pos,
                                    light_direction=c.light_dir, light_color=c.light_color)

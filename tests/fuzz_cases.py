@@ -114,3 +114,43 @@ def make_case(seed: int) -> Case:
                 point=bool(rng.random() < 0.3), light_dir=_light_dir(rng),
                 light_pos=tuple(float(v) for v in centre + rng.normal(size=3) * ext / scale),
                 light_color=tuple(float(v) for v in np.round(rng.uniform(0.0, 2.0, size=3) * 8) / 8), notes=notes)
+
+
+def make_wide_case(seed: int) -> Case:
+    """A scene over several 64^3 regions with empty regions between its blocks (the
+    null-region skip, region advance and entry clip of rayMarchVoxelScene,
+    Renderer.cuh:338-434), seen from up to four scene widths away."""
+    rng = np.random.default_rng(seed)
+    ext = int(rng.choice([200, 320, 500]))
+    lo = rng.integers(-260, 60, size=3)
+    parts, centres = [], []
+    for _ in range(int(rng.integers(2, 7))):
+        size = rng.integers(2, 40, size=3)
+        corner = rng.integers(0, ext - size, size=3)
+        g = np.stack(np.meshgrid(*[np.arange(s) for s in size], indexing="ij"), -1).reshape(-1, 3)
+        keep = rng.random(len(g)) < rng.uniform(0.05, 1.0)
+        parts.append(g[keep] + corner)
+        centres.append(corner + size / 2.0 + lo)
+    parts.append(rng.integers(0, ext, size=(int(rng.integers(0, 3000)), 3)))
+    xyz = (np.concatenate(parts) + lo).astype(np.int32)
+    rgb = rng.integers(0, 1 << 24, size=len(xyz), dtype=np.uint32)
+    scale = int(rng.choice([1, 1, 2, 4]))
+    translation = (0.0, 0.0, 0.0) if rng.random() < 0.5 else \
+        tuple(float(v) for v in np.round(rng.uniform(-9, 9, size=3) * 2) / 2)
+    tr = np.array(translation)
+    centre = (lo + ext / 2.0) / scale + tr
+    d = rng.normal(size=3)
+    d /= np.linalg.norm(d)
+    look = centres[int(rng.integers(0, len(centres)))] / scale + tr
+    if rng.random() < 0.5:                                   # from outside the scene
+        eye = centre + d * rng.uniform(0.6, 4.0) * ext / scale
+    else:                                                    # near a block, across regions
+        eye = look + d * rng.uniform(20.0, 150.0) / scale
+    fwd = look - eye
+    up = (0.0, 0.0, 1.0) if abs(fwd[1]) > 0.95 * np.linalg.norm(fwd) else (0.0, 1.0, 0.0)
+    W, H = int(rng.integers(32, 96)), int(rng.integers(24, 72))
+    return Case(seed=seed, xyz=xyz, rgb=rgb, eye=tuple(float(v) for v in eye), look_at=tuple(float(v) for v in look),
+                up=up, fov=float(rng.uniform(5.0, 70.0)), W=W, H=H, scale=scale, translation=translation,
+                shadows=bool(rng.random() < 0.8), point=bool(rng.random() < 0.3), light_dir=_light_dir(rng),
+                light_pos=tuple(float(v) for v in centre + rng.normal(size=3) * ext / scale),
+                light_color=(1.0, 1.0, 1.0), notes=["wide"])

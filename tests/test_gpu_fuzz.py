@@ -8,7 +8,7 @@ from __future__ import annotations
 import pytest
 
 import oracle
-from tests.fuzz_cases import make_case
+from tests.fuzz_cases import make_case, make_wide_case
 from tests.helpers import oracle_camera_from, oracle_lighting_from
 from tests.test_gpu_parity import ALGOS, STORES, check_frame
 
@@ -17,11 +17,12 @@ pytestmark = pytest.mark.gpu
 vr = pytest.importorskip("voxelraymarcher_amd")
 
 SEEDS = list(range(1000, 1200))
+WIDE_SEEDS = list(range(5000, 5100))
 
 
-@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("seed", SEEDS + WIDE_SEEDS)
 def test_random_views(seed):
-    c = make_case(seed)
+    c = make_wide_case(seed) if seed >= 5000 else make_case(seed)
     cam = vr.Camera(c.eye, c.look_at, c.up, c.fov, c.aspect)
     lit = vr.setup_constant_values(use_shadows=c.shadows, use_point_light=c.point, light_position=c.light_pos,
                                    light_direction=c.light_dir, light_color=c.light_color)
