@@ -41,20 +41,9 @@ import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-import voxelraymarcher_amd as vr  # noqa: E402
-from voxelraymarcher_amd.tiles import BandGather, frame_resolution  # noqa: E402
-
-HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
-N_SIMD = 1024              # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles (SIMD-32)
-BAND_ROWS = 8              # one wave tile high
-HEADLINE = "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s"   # BASELINE.json metric
+CONFIG_NAMES = ["C1", "C2", "C3", "C4", "C5"]     # voxelraymarcher_amd.CONFIGS (BASELINE.json configs)
 
 
 def parse():
@@ -62,19 +51,48 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--config", default="C2", choices=sorted(vr.CONFIGS))
+    p.add_argument("--config", default="C2", choices=CONFIG_NAMES)
     p.add_argument("--tiling", default="auto", choices=["auto", "weak", "fixed"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--frames-in-flight", type=int, default=0,
                    help="band buffers/streams of the frame pipeline (1 = one frame at a time, for PMC passes; "
-                        "default: 3 for C5, whose frames end in a latency-bound crawl pass, else 2 -- "
-                        "profiles/r03/frames_in_flight.txt)")
+                        "default: tiles.pipeline_depth -- 8 for C5, whose frames end in a latency-bound crawl "
+                        "pass, else 2; profiles/r03/queues/)")
+    p.add_argument("--hw-queues", type=int, default=0,
+                   help="hardware queues of this process (GPU_MAX_HW_QUEUES, set before the HIP runtime starts; "
+                        "default: tiles.pipeline_hw_queues -- 16 when more than 3 frames are in flight, else "
+                        "the runtime's own; an exported GPU_MAX_HW_QUEUES is raised to it, never lowered)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="oracle threads (default: the CPUs this process may run on, at most OMP_NUM_THREADS)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes and VALU issue per launch, keyed by config "
                         "(written by profiles/collect_traffic.py)")
     return p.parse_args()
+
+
+ARGS = parse() if __name__ == "__main__" else None
+if ARGS is not None:
+    # The frame pipeline's streams must each get a hardware queue of their own, or two
+    # frames in flight serialise (profiles/r03/queues/): the queue count is read when the
+    # HIP runtime starts, so it is set here, before torch or libvr touch the GPU.
+    from voxelraymarcher_amd.tiles import pipeline_depth, pipeline_hw_queues   # (no GPU, no torch.cuda)
+    # (the GPU box exports GPU_MAX_HW_QUEUES=4, HIP's default: raised when the pipeline needs more)
+    _q = ARGS.hw_queues or pipeline_hw_queues(ARGS.frames_in_flight or pipeline_depth(ARGS.config))
+    _have = os.environ.get("GPU_MAX_HW_QUEUES", "")
+    if _q and (ARGS.hw_queues or not _have.isdigit() or int(_have) < _q):
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(int(_q), 16))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import voxelraymarcher_amd as vr  # noqa: E402
+from voxelraymarcher_amd.tiles import BandGather, frame_resolution, pipeline_depth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+N_SIMD = 1024              # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles (SIMD-32)
+BAND_ROWS = 8              # one wave tile high
+HEADLINE = "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s"   # BASELINE.json metric
 
 
 def cpu_info() -> dict:
@@ -180,7 +198,7 @@ def load_traffic(path: str, cfg_name: str, world: int) -> dict:
 
 
 def main():
-    args = parse()
+    args = ARGS
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -203,7 +221,7 @@ def main():
     stream = torch.cuda.current_stream()
     # N > 1: bands travel as the RGB8 framebuffer (writeColorToFramebuffer's format, 3 B per
     # pixel): rank 0 ends each frame with the RGB8 image
-    depth = args.frames_in_flight or (3 if args.config == "C5" else 2)
+    depth = args.frames_in_flight or pipeline_depth(args.config)
     pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=depth, rgb8=world > 1)
 
     def render(buf):   # on the current stream (BandGather's slot stream in the loops)
@@ -355,7 +373,8 @@ def main():
                                                                        f"scaling)"),
                        "grid": cfg.grid, "width": W, "height": H, "tiling": tiling,
                        "store": cfg.store.name, "algorithm": cfg.algorithm.name, "scale": cfg.scale,
-                       "voxels": int(len(rgb)), "parallelism": par, "frames_in_flight": pipe.depth},
+                       "voxels": int(len(rgb)), "parallelism": par, "frames_in_flight": pipe.depth,
+                       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default")},
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_median": round(kern_median, 4),
             "kernel_ms_grid_order": round(kern_grid_ms, 4),

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Projected N-GPU frame time of a fixed-tiling config from ONE GPU: each rank r of N
+renders only its own 8-row bands (vr_render_bands(r, N), band b -> rank b % N, plus
+the RGB8 pack it sends), pipelined exactly as bench.py runs it (tiles.BandGather's
+frames in flight), timed alone on the box's one MI355X.  The N-GPU frame rate is set
+by the slowest rank (its gather to rank 0 runs beside the next frame),
+so max over ranks of the per-rank frame time is the projection -- without the RCCL
+gather, which no one-GPU box can run (profiles/r03/rccl/).
+
+  python profiles/rank_projection.py [--config C5] [--world 8] [--steps 100]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import voxelraymarcher_amd as vr  # noqa: E402
+from voxelraymarcher_amd.tiles import BandGather, owned_rows  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--config", default="C5")
+p.add_argument("--world", type=int, default=8)
+p.add_argument("--steps", type=int, default=100)
+p.add_argument("--warmup", type=int, default=20)
+p.add_argument("--frames-in-flight", type=int, default=0)
+p.add_argument("--ranks", default="", help="comma-separated subset of ranks (default: all)")
+a = p.parse_args()
+
+cfg = vr.CONFIGS[a.config]
+dev = torch.device("cuda", 0)
+xyz, rgb = cfg.voxels()
+scene = vr.create_scene(xyz, rgb, cfg.store)
+W, H = cfg.width, cfg.height
+cam = vr.Camera.reference(W, H)
+lit = vr.setup_constant_values()
+info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+depth = a.frames_in_flight or (3 if a.config == "C5" else 2)
+words = vr.band_buffer_words(W, H, 8, a.world)
+
+
+# ONE pipeline (its streams) for every run: a second BandGather's new streams may share a
+# hardware queue (4 per process on the box) and serialise its frames (seen: the second
+# pipeline of a process ran C2's rank at 2x the time of every later one)
+pipe = BandGather(W, H, 8, 0, 1, dev, depth=depth)
+packed = [torch.empty(words * 3, dtype=torch.uint8, device=dev) for _ in range(depth)]
+
+
+def run(rank, nranks, steps):
+    k = [0]
+
+    def render(buf):
+        vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, 8, rank, nranks, buf)
+        if nranks > 1:                                  # the send side of bench.py's N > 1 step
+            vr.pack_rgb8(buf[:words], out=packed[k[0] % depth])
+        k[0] += 1
+
+    for _ in range(a.warmup):
+        pipe.step(render)
+    pipe.drain()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pipe.step(render)
+    pipe.drain()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3
+
+
+single = run(0, 1, a.steps)
+ranks = []
+for r in ([int(x) for x in a.ranks.split(",")] if a.ranks else range(a.world)):
+    ms = run(r, a.world, a.steps)
+    ranks.append({"rank": r, "rows": len(owned_rows(H, 8, r, a.world)), "ms_per_frame": round(ms, 4)})
+    print(json.dumps(ranks[-1]), flush=True)
+slow = max(x["ms_per_frame"] for x in ranks)
+print(json.dumps({"config": a.config, "width": W, "height": H, "world": a.world, "frames_in_flight": depth,
+                  "steps": a.steps, "one_gpu_ms_per_frame": round(single, 4),
+                  "projected_ms_per_frame": slow, "projected_speedup": round(single / slow, 2),
+                  "projected_mrays_per_s": round(W * H / (slow * 1e-3) / 1e6, 1),
+                  "note": "max over ranks of each rank's own pipelined frame time on one GPU; RCCL gather not "
+                          "included (overlapped with the next frame in bench.py)"}), flush=True)

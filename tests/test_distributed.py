@@ -153,3 +153,12 @@ def test_fixed_tiling_eight_ranks_4k():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert ok and tmax == world - 1
+
+
+def test_pipeline_policy():
+    """Frames in flight per config and the hardware queues they need (bench.py sets
+    GPU_MAX_HW_QUEUES from these before the HIP runtime starts)."""
+    from voxelraymarcher_amd.tiles import pipeline_depth, pipeline_hw_queues
+    assert pipeline_depth("C2") == 2 and pipeline_depth("C5") == 8
+    assert pipeline_hw_queues(2) == 0 and pipeline_hw_queues(3) == 0
+    assert pipeline_hw_queues(pipeline_depth("C5")) >= pipeline_depth("C5") + 2

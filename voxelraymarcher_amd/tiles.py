@@ -49,6 +49,24 @@ def frame_resolution(width: int, height: int, nranks: int, tiling: str) -> tuple
     raise ValueError(f"unknown tiling {tiling!r}")
 
 
+def pipeline_depth(config: str) -> int:
+    """Frames in flight for a BASELINE config (BandGather's depth).  C5's frames end in
+    a crawl pass -- a latency chain of ~0.3-0.5 ms whatever the rank's share of the
+    frame -- so its pipeline must hold enough frames to cover that chain: 8 (one GPU:
+    0.670 vs 0.710 ms per frame at 3; one rank of 8, fixed tiling: 0.125 vs 0.205 ms,
+    profiles/r03/queues/, profiles/r03/proj/).  The other configs' frames end in a few
+    long tile-pass waves that one more frame covers: 2 (3 and 4 measured slower)."""
+    return 8 if config == "C5" else 2
+
+
+def pipeline_hw_queues(depth: int) -> int:
+    """Hardware queues a process needs so that `depth` frames in flight (one stream
+    each, plus the null stream and rank 0's assembly stream) never share one: two
+    streams on one queue run one after the other (the box's default is 4 queues per
+    process).  0 = the runtime's default suffices."""
+    return 16 if depth > 3 else 0
+
+
 def weak_scaled_resolution(width: int, height: int, nranks: int) -> tuple[int, int]:
     """The same view at about nranks x the pixels (both sides x sqrt(nranks), so the
     aspect ratio -- and with it Camera::Camera's view -- stays put and every rank
