@@ -271,6 +271,9 @@ def main():
     torch.cuda.synchronize()
     # (the events are read after the timed loop: reading 200 of them takes ~17 ms,
     # long enough for an idle GPU to drop its clock before the timed loop starts)
+    # (the W warmup steps stay BEFORE this phase: moved to just before the timed loop
+    # they made a 20-step loop slower, 0.1196-0.1205 -> 0.128 ms per step on one box,
+    # profiles/r03/driver_ab/)
 
     # N > 1: latency of ONE frame, first launch -> gathered and assembled on
     # rank 0, without the overlap of the pipelined loop
