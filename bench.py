@@ -77,7 +77,8 @@ if ARGS is not None:
     # HIP runtime starts, so it is set here, before torch or libvr touch the GPU.
     from voxelraymarcher_amd.tiles import pipeline_depth, pipeline_hw_queues   # (no GPU, no torch.cuda)
     # (the GPU box exports GPU_MAX_HW_QUEUES=4, HIP's default: raised when the pipeline needs more)
-    _q = ARGS.hw_queues or pipeline_hw_queues(ARGS.frames_in_flight or pipeline_depth(ARGS.config))
+    _q = ARGS.hw_queues or pipeline_hw_queues(ARGS.frames_in_flight or pipeline_depth(ARGS.config),
+                                              int(os.environ.get("WORLD_SIZE", "1")))
     _have = os.environ.get("GPU_MAX_HW_QUEUES", "")
     if _q and (ARGS.hw_queues or not _have.isdigit() or int(_have) < _q):
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(int(_q), 16))

@@ -162,3 +162,5 @@ def test_pipeline_policy():
     assert pipeline_depth("C2") == 2 and pipeline_depth("C5") == 8
     assert pipeline_hw_queues(2) == 0 and pipeline_hw_queues(3) == 0
     assert pipeline_hw_queues(pipeline_depth("C5")) >= pipeline_depth("C5") + 2
+    # N > 1: rank 0's assembly stream and the RCCL stream join the two frame streams
+    assert pipeline_hw_queues(2, 8) >= 2 + 3

@@ -59,12 +59,14 @@ def pipeline_depth(config: str) -> int:
     return 8 if config == "C5" else 2
 
 
-def pipeline_hw_queues(depth: int) -> int:
-    """Hardware queues a process needs so that `depth` frames in flight (one stream
-    each, plus the null stream and rank 0's assembly stream) never share one: two
+def pipeline_hw_queues(depth: int, nranks: int = 1) -> int:
+    """Hardware queues a process needs so that its busy streams never share one: two
     streams on one queue run one after the other (the box's default is 4 queues per
-    process).  0 = the runtime's default suffices."""
-    return 16 if depth > 3 else 0
+    process; measured: C5 at 4 frames in flight on 4 queues ran slower than at 3).  The
+    streams: one per frame in flight, the null stream, and with N > 1 ranks rank 0's
+    assembly stream and the RCCL communicator's stream.  0 = the default suffices."""
+    streams = depth + 1 + (2 if nranks > 1 else 0)
+    return 16 if streams > 4 else 0
 
 
 def weak_scaled_resolution(width: int, height: int, nranks: int) -> tuple[int, int]:
