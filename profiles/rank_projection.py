@@ -29,6 +29,7 @@ p.add_argument("--steps", type=int, default=100)
 p.add_argument("--warmup", type=int, default=20)
 p.add_argument("--frames-in-flight", type=int, default=0)
 p.add_argument("--ranks", default="", help="comma-separated subset of ranks (default: all)")
+p.add_argument("--band-rows", type=int, default=8)
 a = p.parse_args()
 
 cfg = vr.CONFIGS[a.config]
@@ -40,13 +41,14 @@ cam = vr.Camera.reference(W, H)
 lit = vr.setup_constant_values()
 info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
 depth = a.frames_in_flight or (3 if a.config == "C5" else 2)
-words = vr.band_buffer_words(W, H, 8, a.world)
+B = a.band_rows
+words = vr.band_buffer_words(W, H, B, a.world)
 
 
 # ONE pipeline (its streams) for every run: a second BandGather's new streams may share a
 # hardware queue (4 per process on the box) and serialise its frames (seen: the second
 # pipeline of a process ran C2's rank at 2x the time of every later one)
-pipe = BandGather(W, H, 8, 0, 1, dev, depth=depth)
+pipe = BandGather(W, H, B, 0, 1, dev, depth=depth)
 packed = [torch.empty(words * 3, dtype=torch.uint8, device=dev) for _ in range(depth)]
 
 
@@ -54,7 +56,7 @@ def run(rank, nranks, steps):
     k = [0]
 
     def render(buf):
-        vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, 8, rank, nranks, buf)
+        vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, B, rank, nranks, buf)
         if nranks > 1:                                  # the send side of bench.py's N > 1 step
             vr.pack_rgb8(buf[:words], out=packed[k[0] % depth])
         k[0] += 1
@@ -75,10 +77,11 @@ single = run(0, 1, a.steps)
 ranks = []
 for r in ([int(x) for x in a.ranks.split(",")] if a.ranks else range(a.world)):
     ms = run(r, a.world, a.steps)
-    ranks.append({"rank": r, "rows": len(owned_rows(H, 8, r, a.world)), "ms_per_frame": round(ms, 4)})
+    ranks.append({"rank": r, "rows": len(owned_rows(H, B, r, a.world)), "ms_per_frame": round(ms, 4)})
     print(json.dumps(ranks[-1]), flush=True)
 slow = max(x["ms_per_frame"] for x in ranks)
-print(json.dumps({"config": a.config, "width": W, "height": H, "world": a.world, "frames_in_flight": depth,
+print(json.dumps({"config": a.config, "width": W, "height": H, "world": a.world, "band_rows": B,
+                  "frames_in_flight": depth,
                   "steps": a.steps, "one_gpu_ms_per_frame": round(single, 4),
                   "projected_ms_per_frame": slow, "projected_speedup": round(single / slow, 2),
                   "projected_mrays_per_s": round(W * H / (slow * 1e-3) / 1e6, 1),
