@@ -624,9 +624,12 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     SlotRing::Dev& D = lease.D();
     SlotRing::Dev::Order& O = D.ord[lease.idx];
     bool remake = false;
-    bool heavy = schedule == VR_SCHEDULE_HEAVIEST_FIRST;
-    if (schedule == VR_SCHEDULE_AUTO)       // (the lock orders launches: "previous" is well defined)
-        heavy = !D.any || D.last_stream == st || hipEventQuery(D.ev[D.last_idx]) == hipSuccess;
+    // (the lock orders launches: "previous" is well defined)
+    const bool alone = !D.any || D.last_stream == st || hipEventQuery(D.ev[D.last_idx]) == hipSuccess;
+    bool heavy = schedule == VR_SCHEDULE_HEAVIEST_FIRST || (schedule == VR_SCHEDULE_AUTO && alone);
+    // crawl records per wave: a lone frame ends with the crawl pass's longest chain (4 per
+    // wave); with frames in flight the pass's issue cycles are what count (8 per wave)
+    v.crawl_rpw = alone ? 4u : 8u;
     D.any = true;
     D.last_stream = st;
     D.last_idx = lease.idx;
@@ -652,7 +655,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         remake = !match || ++O.age >= order_refresh();
         v.cost = remake ? O.cost : nullptr;
     }
-    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st, vr::crawl_grid(expect));
+    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st, vr::crawl_grid(expect, v.crawl_rpw));
     if (e == hipSuccess && remake) {
         // (on a side stream instead -- one more stream than the box's 4 hardware queues
         // serialised the two render streams: C2 0.1124 -> 0.1277 ms per frame in flight,

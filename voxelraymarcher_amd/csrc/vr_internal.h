@@ -92,6 +92,7 @@ struct KView {
     uint32_t* defer;          // crawl deferral slot: [count, done, overflow, 0, records (kDeferRecWords each)...]
     uint32_t defer_cap;
     uint32_t crawl_rewalk;    // 1: deferred crawls are walked from the pixel's start (VR_KERNEL_TILE_REWALK)
+    uint32_t crawl_rpw;       // crawl records per wave (0 = 4): 4 for a lone frame, 8 with frames in flight
     uint32_t* defer_stat;     // host-mapped word: the crawl pass writes its record count there (grid sizing)
     // Tile-pass work order ("Heaviest tiles first"): workgroup i of the grid
     // renders tile order[i] = (tile row << 16 | tile column) -- a permutation of the grid
@@ -125,7 +126,7 @@ constexpr uint32_t kDeferWords = 4 + kDeferCap * kDeferRecWords;
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,
                         hipStream_t stream, uint32_t crawl_wgs);
 // Crawl-pass grid for a launch that expects about `records` deferred pixels.
-uint32_t crawl_grid(uint32_t records);
+uint32_t crawl_grid(uint32_t records, uint32_t rpw);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);
 // The tile pass's grid for a view (columns, rows of workgroups) and its waves per workgroup.
 void march_grid(const KView& v, uint32_t& columns, uint32_t& rows);

@@ -1537,9 +1537,13 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     // kCrawlRpw records per wave at a time (lanes 0 .. kCrawlRpw-1): each record is a long
     // chain of dependent iterations, and the lanes of a wave take different paths through
     // the walk, so fewer lanes per wave -- spread over more waves -- finish sooner
+    // (v.crawl_rpw: the host's choice per launch -- 4 for a lone frame, whose time is the
+    // longest record's chain; 8 with frames in flight, where the pass's issue cycles count:
+    // C5 0.6707 -> 0.6514 ms per frame, profiles/r03/rpw_deep/)
+    const uint32_t rpw = v.crawl_rpw ? v.crawl_rpw : kCrawlRpw;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, wlane = threadIdx.x & 63u;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t i = wave * kCrawlRpw + wlane; wlane < kCrawlRpw && i < n; i += nwaves * kCrawlRpw) {
+    for (uint32_t i = wave * rpw + wlane; wlane < rpw && i < n; i += nwaves * rpw) {
         uint32_t* r = v.defer + 4 + (size_t)i * kDeferRecWords;
         uint32_t b;
         const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
@@ -1607,9 +1611,10 @@ __global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __rest
 // flight, profiles/r03/ab_crawl_rpw.txt), at least 64 workgroups.  The host sizes it from
 // the count an earlier launch of the device wrote to defer_stat: a launch that defers
 // nothing (C2-C4) keeps the small grid (1024 empty workgroups cost C2 0.6 %).
-uint32_t crawl_grid(uint32_t records) {
+uint32_t crawl_grid(uint32_t records, uint32_t rpw) {
     const uint32_t waves_per_wg = kTilesX * kTilesY;
-    const uint64_t waves = ((uint64_t)records * 5u / 4u + kCrawlRpw - 1u) / kCrawlRpw;
+    rpw = rpw ? rpw : kCrawlRpw;
+    const uint64_t waves = ((uint64_t)records * 5u / 4u + rpw - 1u) / rpw;
     const uint64_t wgs = (waves + waves_per_wg - 1u) / waves_per_wg;
     return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(wgs, 64u), 4096u);
 }
