@@ -60,35 +60,52 @@ def parse():
                         "pass, else 2; profiles/r03/queues/)")
     p.add_argument("--hw-queues", type=int, default=0,
                    help="hardware queues of this process (GPU_MAX_HW_QUEUES, set before the HIP runtime starts; "
-                        "default: tiles.pipeline_hw_queues -- 16 when more than 3 frames are in flight, else "
-                        "the runtime's own; an exported GPU_MAX_HW_QUEUES is raised to it, never lowered)")
+                        "at most 16).  Default: tiles.pipeline_hw_queues -- 16 when the pipeline's streams "
+                        "outnumber the runtime's 4 queues -- and an exported GPU_MAX_HW_QUEUES is raised to "
+                        "that, never lowered; an explicit --hw-queues sets it as given (clamped to 16, the "
+                        "line records requested and effective counts)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="oracle threads (default: the CPUs this process may run on, at most OMP_NUM_THREADS)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes and VALU issue per launch, keyed by config "
                         "(written by profiles/collect_traffic.py)")
+    p.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                   help="N > 1 process group: auto/nccl = RCCL over xGMI (one GPU per rank); gloo = the same "
+                        "pipeline with the gather staged through host memory (tiles.init_frame_group)")
+    p.add_argument("--same-device", action="store_true",
+                   help="every rank on cuda:0 (rehearse N ranks on a one-GPU box; needs --backend gloo)")
+    p.add_argument("--resolution", default="",
+                   help="WxH instead of the config's frame (tests; the same view and scene)")
+    p.add_argument("--dump-frame", default="",
+                   help="rank 0 saves the last frame of the timed loop (.npy): RGB8 [H, W, 3] with N > 1 ranks, "
+                        "packed 0x00RRGGBB words [H, W] with one")
     return p.parse_args()
 
 
 ARGS = parse() if __name__ == "__main__" else None
+HW_QUEUES_REQUESTED = None
 if ARGS is not None:
     # The frame pipeline's streams must each get a hardware queue of their own, or two
     # frames in flight serialise (profiles/r03/queues/): the queue count is read when the
     # HIP runtime starts, so it is set here, before torch or libvr touch the GPU.
     from voxelraymarcher_amd.tiles import pipeline_depth, pipeline_hw_queues   # (no GPU, no torch.cuda)
-    # (the GPU box exports GPU_MAX_HW_QUEUES=4, HIP's default: raised when the pipeline needs more)
-    _q = ARGS.hw_queues or pipeline_hw_queues(ARGS.frames_in_flight or pipeline_depth(ARGS.config),
-                                              int(os.environ.get("WORLD_SIZE", "1")))
+    # (the GPU box exports GPU_MAX_HW_QUEUES=4, HIP's default: raised when the pipeline needs more;
+    # ranks sharing one GPU (--same-device) keep the default: their queues add up on one device)
+    _q = ARGS.hw_queues or (0 if ARGS.same_device else
+                            pipeline_hw_queues(ARGS.frames_in_flight or pipeline_depth(ARGS.config),
+                                               int(os.environ.get("WORLD_SIZE", "1"))))
     _have = os.environ.get("GPU_MAX_HW_QUEUES", "")
     if _q and (ARGS.hw_queues or not _have.isdigit() or int(_have) < _q):
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(int(_q), 16))
+        if ARGS.hw_queues and ARGS.hw_queues > 16:
+            HW_QUEUES_REQUESTED = ARGS.hw_queues
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import voxelraymarcher_amd as vr  # noqa: E402
-from voxelraymarcher_amd.tiles import BandGather, frame_resolution, pipeline_depth  # noqa: E402
+from voxelraymarcher_amd.tiles import BandGather, frame_resolution, init_frame_group, pipeline_depth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 N_SIMD = 1024              # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles (SIMD-32)
@@ -206,16 +223,25 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    dev, backend, stage_host = init_frame_group(world, local, args.backend, args.same_device)
+
+    def allreduce(x: float | int, op=dist.ReduceOp.SUM, dtype=torch.float64):
+        """A scalar over the ranks (host tensors for gloo, device tensors for RCCL)."""
+        t = torch.tensor([x], dtype=dtype, device="cpu" if stage_host else dev)
+        if world > 1:
+            dist.all_reduce(t, op=op)
+        return t.item()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
 
     cfg = vr.CONFIGS[args.config]
     tiling = args.tiling if args.tiling != "auto" else ("fixed" if cfg.name == "C5" else "weak")
     xyz, rgb = cfg.voxels()
-    scene = vr.create_scene(xyz, rgb, cfg.store, device=local)
-    W, H = frame_resolution(cfg.width, cfg.height, world, tiling)
+    scene = vr.create_scene(xyz, rgb, cfg.store, device=dev.index)
+    W0, H0 = (int(v) for v in args.resolution.lower().split("x")) if args.resolution else (cfg.width, cfg.height)
+    W, H = frame_resolution(W0, H0, world, tiling)
     cam = vr.Camera.reference(W, H)
     lit = vr.setup_constant_values()
     info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
@@ -223,21 +249,25 @@ def main():
     # N > 1: bands travel as the RGB8 framebuffer (writeColorToFramebuffer's format, 3 B per
     # pixel): rank 0 ends each frame with the RGB8 image
     depth = args.frames_in_flight or pipeline_depth(args.config)
-    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=depth, rgb8=world > 1)
+    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=depth, rgb8=world > 1, stage_host=stage_host)
 
     def render(buf):   # on the current stream (BandGather's slot stream in the loops)
         vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, rank, world, buf)
 
     # algorithmic bytes of THIS rank's launch (its bands; instrumented kernel,
-    # untimed) and of the whole frame (sum over ranks)
+    # untimed) and of the whole frame (sum over ranks); `stats`: the part of
+    # them the crawl pass credits for crawl iterations it fast-forwards in closed form
+    # (their existence reads are counted, never issued)
     ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    stats = torch.zeros(2, dtype=torch.int64, device=dev)
     vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, pipe.bufs[0], band_rows=BAND_ROWS, rank=rank,
-                 nranks=world, counter=ctr)
+                 nranks=world, counter=ctr, stats=stats)
     torch.cuda.synchronize()
     launch_bytes = int(ctr.item())
-    if world > 1:
-        dist.all_reduce(ctr)
-    frame_bytes = int(ctr.item())
+    ff_iters, ff_bytes = (int(x) for x in stats.cpu().tolist())
+    issued_bytes = launch_bytes - ff_bytes
+    frame_bytes = int(allreduce(launch_bytes, dtype=torch.int64))
+    frame_issued = int(allreduce(issued_bytes, dtype=torch.int64))
 
     for _ in range(args.warmup):
         pipe.step(render)
@@ -282,51 +312,76 @@ def main():
     if world > 1:
         lat = []
         for _ in range(5):
-            dist.barrier()
+            barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             pipe.step(render)
             pipe.drain()
             torch.cuda.synchronize()
             lat.append(time.perf_counter() - t0)
-        frame_latency_ms = float(np.median(lat)) * 1e3
+        frame_latency_ms = allreduce(float(np.median(lat)) * 1e3, op=dist.ReduceOp.MAX)
 
-    if world > 1:
-        dist.barrier()
+    # the timed loop; each launch is also bracketed by HIP events on its own stream (the
+    # slot stream BandGather renders on): launch_ms_timed, the roofline's duration
+    ev_t = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    it_t = iter(ev_t)
+
+    def render_timed(buf):
+        a, b = next(it_t)
+        a.record()
+        render(buf)
+        b.record()
+
+    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        pipe.step(render)
+        pipe.step(render_timed)
     pipe.drain()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
+    dt = allreduce(dt, op=dist.ReduceOp.MAX)
     ms_per_step = dt / args.steps * 1e3
     kern_all = [a.elapsed_time(b) for a, b in ev]
     kern_ms = float(np.mean(kern_all))
     kern_median = float(np.median(kern_all))
     kern_grid_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_grid]))
+    launch_ms_timed = float(np.mean([a.elapsed_time(b) for a, b in ev_t]))
     mrays = W * H / (ms_per_step * 1e-3) / 1e6
+    if args.dump_frame and rank == 0:
+        np.save(args.dump_frame, pipe.last_frame().cpu().numpy())
 
     if rank == 0:
-        achieved_isolated = launch_bytes / (kern_ms * 1e-3) / 1e9
-        achieved_pipe = launch_bytes / (ms_per_step * 1e-3) / 1e9    # this GPU's launches overlap in the loop
+        def gbs(nbytes, ms):
+            return nbytes / (ms * 1e-3) / 1e9
+        # The roofline's numerator: the bytes this launch's walks stand for minus
+        # the existence reads of crawl iterations the crawl pass fast-forwards in closed form
+        # (it never issues them); its duration: the launch's own, timed in the timed loop.
+        achieved = gbs(issued_bytes, launch_ms_timed)
         tj = load_traffic(args.traffic_json, cfg.name, world)
         traffic = tj.get("hbm_bytes_per_launch")
-        roof = {"bound": None, "achieved": round(achieved_isolated, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved_isolated / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "achieved_basis": "algorithmic bytes per launch (SURVEY 8(d): the words the reference walk reads, "
-                                  "counted by the instrumented kernel) / the launch's average duration (kernel_ms, "
-                                  "HIP events on the launch stream) -- the north star's figure, mostly served "
-                                  "from L2/MALL, not HBM",
-                "achieved_pipelined": round(achieved_pipe, 1),
-                "frac_pipelined": round(achieved_pipe / HBM_PEAK_GBS, 4),
-                "algorithmic_bytes_per_launch": launch_bytes, "algorithmic_bytes_per_frame": frame_bytes}
+        roof = {"bound": None, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "achieved_basis": "algorithmic bytes issued per launch (SURVEY 8(d): the words the reference walk "
+                                  "reads, counted by the instrumented kernel, minus the existence reads of crawl "
+                                  "iterations fast-forwarded in closed form) / the launch's mean duration in the "
+                                  "timed loop (launch_ms_timed: tile pass + crawl pass, HIP events on the launch's "
+                                  "stream) -- mostly served from L2/MALL, not HBM",
+                "launch_ms_timed": round(launch_ms_timed, 4),
+                "algorithmic_bytes_per_launch": launch_bytes,
+                "algorithmic_bytes_issued_per_launch": issued_bytes,
+                "crawl_iterations_fast_forwarded": ff_iters,
+                "algorithmic_bytes_per_frame": frame_bytes, "algorithmic_bytes_issued_per_frame": frame_issued,
+                "frac_grid_order": round(gbs(issued_bytes, kern_grid_ms) / HBM_PEAK_GBS, 4),
+                "frac_learned_order": round(gbs(issued_bytes, kern_ms) / HBM_PEAK_GBS, 4),
+                "frac_pipelined": round(gbs(issued_bytes, ms_per_step) / HBM_PEAK_GBS, 4),
+                "frac_section8d": round(gbs(launch_bytes, launch_ms_timed) / HBM_PEAK_GBS, 4),
+                "fracs_basis": "the same issued bytes over: kernel_ms_grid_order (one launch alone in grid order, "
+                               "as a first render), kernel_ms (alone, heaviest tile groups first from an earlier "
+                               "launch's costs), ms_per_step (the pipelined frame rate); frac_section8d: the full "
+                               "SURVEY 8(d) count over launch_ms_timed",
+                }
         hbm_frac = valu_frac = None
         if traffic:
             # what HBM actually serves (PMC DRAM bytes per launch, profiles/)
@@ -357,7 +412,9 @@ def main():
         metric = HEADLINE if cfg.name == "C2" else \
             (f"Mrays/sec at {cfg.width}x{cfg.height}, {cfg.grid}^3 grid ({cfg.store.name}+{cfg.algorithm.name}); "
              f"achieved HBM GB/s")
-        par = f"row-band tiles x{world}" + (" + RCCL gather of the RGB8 bands to rank 0 (overlapped with the "
+        gather = ("RCCL gather" if backend == "nccl" else "gloo gather staged through host memory") + \
+            (" (ranks sharing cuda:0)" if args.same_device else "")
+        par = f"row-band tiles x{world}" + (f" + {gather} of the RGB8 bands to rank 0 (overlapped with the "
                                              "next frame)" if world > 1 else "")
         line = {
             "metric": metric,
@@ -382,11 +439,19 @@ def main():
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_median": round(kern_median, 4),
             "kernel_ms_grid_order": round(kern_grid_ms, 4),
-            "kernel_ms_basis": "one launch at a time on one stream (AUTO schedule: heaviest tile groups first); "
-                               "kernel_ms_grid_order: the same launches in grid order, as the pipelined loop runs them",
+            "kernel_ms_basis": "one launch at a time on one stream (AUTO schedule: heaviest tile groups first, "
+                               "learned from earlier launches of the same view); kernel_ms_grid_order: the same "
+                               "launches in grid order (a first render); roofline.launch_ms_timed: the launches "
+                               "of the timed loop (frames in flight, grid order)",
             "kernel_mrays_per_s": round(W * H / world / (kern_ms * 1e-3) / 1e6, 2),
             "roofline": roof,
+            # the non-instrumented launches of this run in order, per phase (a rocprofv3 kernel
+            # trace of the same command splits into them: profiles/roofline_phases.py)
+            "dispatch_phases": {"warmup": args.warmup, "untimed": 40, "iso_grid": n_iso, "iso_learned": n_iso,
+                                "latency": 5 if world > 1 else 0, "timed": args.steps},
         }
+        if HW_QUEUES_REQUESTED is not None:
+            line["config"]["hw_queues_requested"] = HW_QUEUES_REQUESTED
         if frame_latency_ms is not None:
             line["frame_latency_ms"] = round(frame_latency_ms, 4)
         if world == 1 and not args.no_cpu_baseline:

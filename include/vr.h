@@ -165,17 +165,39 @@ typedef enum {
  * rows [row_begin,row_end) of the frame cut into bands of band_rows rows,
  * band b rendered when b % nranks == rank; out_dev gets this rank's bands
  * packed as in vr_render_bands.  bytes_dev (optional, device uint64,
- * caller-zeroed) accumulates the SURVEY.md 8(d) algorithmic bytes. */
+ * caller-zeroed) accumulates the SURVEY.md 8(d) algorithmic bytes.
+ *
+ * Versioned by its leading size: set struct_size = sizeof(vr_render_opts)
+ * (vr_render_opts_init does, with every other field at its default).  The
+ * library rejects (VR_E_INVALID) a struct_size below VR_RENDER_OPTS_MIN_SIZE --
+ * the layout before this field existed began with `kernel` (0..3), so a caller
+ * built against it is refused instead of having fields read past its struct --
+ * and treats fields that lie past struct_size as zero (callers built against
+ * an older, shorter version of this layout keep working). */
 typedef struct {
+    uint32_t struct_size; /* sizeof(vr_render_opts) as the caller was compiled */
     uint32_t kernel;      /* vr_kernel */
     uint32_t row_begin, row_end;
     uint32_t band_rows;   /* 0 = one band covering [row_begin,row_end) */
     uint32_t rank, nranks;
-    uint64_t* bytes_dev;
     uint32_t defer_cap;   /* records in the crawl pass's deferral list: 0 = the default (16384);
                              smaller values exercise its overflow path (tests) */
+    uint64_t* bytes_dev;
     uint32_t schedule;    /* vr_schedule: the tile pass's work order (pixels never depend on it) */
+    uint32_t reserved;    /* 0 */
+    /* (optional, device uint64[2], caller-zeroed; read only with bytes_dev) the part of
+     * bytes_dev's count that the kernels credit without loading it: [0] cluster-skip crawl
+     * iterations fast-forwarded in closed form (Renderer.cuh:290-306, performVoxelSpaceJump
+     * :707-725), [1] their existence-read bytes (4 each).  bytes_dev - [1] = the bytes the
+     * walk's own reads stand for. */
+    uint64_t* stats_dev;
 } vr_render_opts;
+/* The smallest struct_size accepted: the layout up to and including `reserved`. */
+#define VR_RENDER_OPTS_MIN_SIZE 48u
+
+/* Defaults: struct_size = sizeof(vr_render_opts), kernel AUTO, rows [0, UINT32_MAX) --
+ * clipped to the frame by the render call -- one band, rank 0 of 1, schedule AUTO. */
+int vr_render_opts_init(vr_render_opts* opts);
 
 /* Work order of the tile pass.  A frame's time alone is set by its slowest tiles:
  * dispatched heaviest first (costs recorded by an earlier launch of the same grid

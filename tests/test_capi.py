@@ -43,8 +43,35 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     assert ctypes.sizeof(_capi.VrCamera) == 60
     assert ctypes.sizeof(_capi.VrLighting) == 44
-    assert ctypes.sizeof(_capi.VrRenderOpts) == 40
+    assert ctypes.sizeof(_capi.VrRenderOpts) == 56
+    assert _capi.VrRenderOpts.reserved.offset + 4 == _capi.VR_RENDER_OPTS_MIN_SIZE
     assert ctypes.sizeof(_capi.VrSynthParams) == 40
+    assert f"#define VR_RENDER_OPTS_MIN_SIZE {_capi.VR_RENDER_OPTS_MIN_SIZE}u" in open(
+        os.path.join(ROOT, "include", "vr.h")).read()
+
+
+def test_render_opts_versioning():
+    """vr_render_opts carries its size (include/vr.h): vr_render_opts_init fills it, and a
+    struct laid out as before the field existed (its first word is `kernel`, 0..3) is
+    refused with VR_E_INVALID before any other argument is looked at -- no field is read
+    past the caller's struct."""
+    o = _capi.VrRenderOpts()
+    _capi.check(vr.lib().vr_render_opts_init(ctypes.byref(o)), "init")
+    assert o.struct_size == ctypes.sizeof(o) and o.nranks == 1 and o.row_end == 0xFFFFFFFF
+    assert (o.kernel, o.schedule, o.defer_cap, o.reserved) == (0, 0, 0, 0) and not o.bytes_dev and not o.stats_dev
+
+    class OldOpts(ctypes.Structure):      # the round-3 layout
+        _fields_ = [("kernel", ctypes.c_uint32), ("row_begin", ctypes.c_uint32), ("row_end", ctypes.c_uint32),
+                    ("band_rows", ctypes.c_uint32), ("rank", ctypes.c_uint32), ("nranks", ctypes.c_uint32),
+                    ("bytes_dev", ctypes.c_void_p), ("defer_cap", ctypes.c_uint32), ("schedule", ctypes.c_uint32)]
+    old = OldOpts(3, 0, 16, 8, 0, 1, None, 0, 0)
+    lib = vr.lib()
+    rc = lib.vr_render_ex(None, 1, None, None, None, 1, 16, 16, ctypes.cast(ctypes.byref(old),
+                          ctypes.POINTER(_capi.VrRenderOpts)), None, None)
+    assert rc == -1 and b"struct_size" in lib.vr_last_error()
+    o.reserved = 1
+    assert lib.vr_render_ex(None, 1, None, None, None, 1, 16, 16, ctypes.byref(o), None, None) == -1
+    assert b"reserved" in lib.vr_last_error()
 
 
 @pytest.mark.parametrize("W,H", [(1920, 1080), (256, 256), (3840, 2160), (97, 41)])

@@ -1,10 +1,11 @@
-"""GPU test of the per-launch scratch slots (vr_host.cpp SlotRing): the
-crawl pass's deferral list, and the crawl pass's own high-priority stream
-fenced by per-slot events.  Many launches in flight on several streams at
-once, far more of them than the ring has slots, must each render exactly the
-frame one serial launch renders: a slot shared by two launches in flight would
-mix their deferred records (wrong or zero pixels), and a missing fence would
-let a frame be read before its crawl pass wrote it."""
+"""GPU test of the per-launch scratch slots (vr_host.cpp SlotRing): each slot's
+crawl-pass deferral list and its work-order buffers, fenced by per-slot events;
+both passes of a launch run on the launch's own stream (with launches in flight
+the crawl pass takes 8 records per wave).  Many launches in flight on several
+streams at once, far more of them than the ring has slots, must each render
+exactly the frame one serial launch renders: a slot shared by two launches in
+flight would mix their deferred records (wrong or zero pixels), and a missing
+fence would let a frame be read before its crawl pass wrote it."""
 from __future__ import annotations
 
 import numpy as np

@@ -185,11 +185,20 @@ struct Ctx {
     uint32_t iters = 0;
     bool aborted = false;
     uint32_t bytes = 0;
+    uint32_t ff = 0;     // (COUNT) crawl iterations credited in closed form (crawl_run)
 
     __device__ Ctx(const KScene& s_, const KView& v_) : s(s_), v(v_) {}
 
     __device__ __forceinline__ void count(uint32_t b) {
         if (COUNT) bytes += b;
+    }
+    // n crawl iterations fast-forwarded: the existence read each of them stands for
+    //  is credited, but the kernel never issues it
+    __device__ __forceinline__ void count_ff(uint32_t n) {
+        if (COUNT) {
+            bytes += 4u * n;
+            ff += n;
+        }
     }
     __device__ __forceinline__ bool tick() {
         if (aborted) return false;

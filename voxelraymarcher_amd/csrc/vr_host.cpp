@@ -627,6 +627,11 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // (the lock orders launches: "previous" is well defined)
     const bool alone = !D.any || D.last_stream == st || hipEventQuery(D.ev[D.last_idx]) == hipSuccess;
     bool heavy = schedule == VR_SCHEDULE_HEAVIEST_FIRST || (schedule == VR_SCHEDULE_AUTO && alone);
+    // A launch captured into a graph renders in grid order: the order's host-side
+    // bookkeeping (age, remake) would not replay with the graph, and its buffers are
+    // stream-ordered allocations.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) heavy = false;
     // crawl records per wave: a lone frame ends with the crawl pass's longest chain (4 per
     // wave); with frames in flight the pass's issue cycles are what count (8 per wave)
     v.crawl_rpw = alone ? 4u : 8u;
@@ -635,16 +640,21 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     D.last_idx = lease.idx;
     if (heavy && order_enabled() && n != 0) {
         if (n > O.cap) {
-            // grow (the slot's previous launch is fenced on this stream; free waits for it)
-            hipError_t e = hipStreamSynchronize(st);
-            if (e == hipSuccess && O.cost) e = hipFree(O.cost);
-            if (e == hipSuccess && O.order) e = hipFree(O.order);
+            // Grow, stream-ordered: the slot's previous launch -- the last user of the old
+            // buffers -- is fenced on this stream (SlotLease::acquire), so freeing them on
+            // it needs no host synchronisation.  Every path frees what it allocated.
+            hipError_t e = hipSuccess;
+            if (O.cost) e = hipFreeAsync(O.cost, st);
+            if (O.order) {
+                const hipError_t e2 = hipFreeAsync(O.order, st);
+                if (e == hipSuccess) e = e2;
+            }
             O = SlotRing::Dev::Order{};
-            if (e == hipSuccess) e = hipMalloc((void**)&O.cost, sizeof(uint32_t) * vr::kWavesPerTileGroup * (size_t)n);
-            if (e == hipSuccess) e = hipMalloc((void**)&O.order, sizeof(uint32_t) * (size_t)n);
+            if (e == hipSuccess) e = hipMallocAsync((void**)&O.cost, sizeof(uint32_t) * vr::kWavesPerTileGroup * (size_t)n, st);
+            if (e == hipSuccess) e = hipMallocAsync((void**)&O.order, sizeof(uint32_t) * (size_t)n, st);
             if (e != hipSuccess) {
-                if (O.cost) (void)hipFree(O.cost);
-                if (O.order) (void)hipFree(O.order);
+                if (O.cost) (void)hipFreeAsync(O.cost, st);
+                if (O.order) (void)hipFreeAsync(O.order, st);
                 O = SlotRing::Dev::Order{};
                 return hip_fail(e, "work order buffers");
             }
@@ -971,33 +981,69 @@ void vr_scene_destroy(vr_scene* s) {
 int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
                  const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
                  const vr_render_opts* opts, uint32_t* out_dev, void* stream) {
+    if (!opts) return fail(VR_E_INVALID, "opts is NULL");
+    // Versioned struct (vr.h): a caller built before struct_size existed passes `kernel`
+    // (0..3) in the first word and is refused; fields past the caller's struct read as 0.
+    // (checked first: only the caller's own struct_size bytes are ever read)
+    if (opts->struct_size < VR_RENDER_OPTS_MIN_SIZE)
+        return fail(VR_E_INVALID, "vr_render_opts.struct_size is " + std::to_string(opts->struct_size) +
+                                      ": set it to sizeof(vr_render_opts) (vr_render_opts_init); a struct built "
+                                      "against the layout without struct_size is not accepted");
+    vr_render_opts o{};
+    std::memcpy(&o, opts, std::min<size_t>(opts->struct_size, sizeof o));
+    if (o.reserved != 0u) return fail(VR_E_INVALID, "vr_render_opts.reserved must be 0");
     vr::KView v;
     int rc = make_view(s, cam, lit, translation, scale, width, height, v);
     if (rc) return rc;
-    if (!opts) return fail(VR_E_INVALID, "opts is NULL");
     if (!out_dev) return fail(VR_E_INVALID, "out_dev is NULL");
-    if (opts->row_begin > opts->row_end || opts->row_end > height) return fail(VR_E_INVALID, "bad row range");
-    if (!opts->nranks || opts->rank >= opts->nranks) return fail(VR_E_INVALID, "bad band partition");
-    const uint32_t rows = opts->row_end - opts->row_begin;
-    const uint32_t band = opts->band_rows ? opts->band_rows : std::max(1u, rows);
-    v.row0 = opts->row_begin;
-    v.row_limit = opts->row_end;
+    const uint32_t row_end = o.row_end == 0xFFFFFFFFu ? height : o.row_end;
+    if (o.row_begin > row_end || row_end > height) return fail(VR_E_INVALID, "bad row range");
+    if (!o.nranks || o.rank >= o.nranks) return fail(VR_E_INVALID, "bad band partition");
+    const uint32_t rows = row_end - o.row_begin;
+    const uint32_t band = o.band_rows ? o.band_rows : std::max(1u, rows);
+    v.row0 = o.row_begin;
+    v.row_limit = row_end;
     v.band_rows = band;
     v.band_minv = band == 1u ? 0xFFFFFFFFu : (uint32_t)((1ull << 32) / band);
-    v.rank = opts->rank;
-    v.nranks = opts->nranks;
-    v.local_rows = (uint32_t)(vr_band_buffer_words(width, rows, band, opts->nranks) / width);
+    v.rank = o.rank;
+    v.nranks = o.nranks;
+    v.local_rows = (uint32_t)(vr_band_buffer_words(width, rows, band, o.nranks) / width);
     v.out = out_dev;
-    v.bytes = (unsigned long long*)opts->bytes_dev;
-    v.defer_cap = opts->defer_cap;
-    if (opts->schedule > VR_SCHEDULE_HEAVIEST_FIRST) return fail(VR_E_INVALID, "unknown schedule");
-    return launch(s, algo, opts->kernel, opts->schedule, v, stream);
+    v.bytes = (unsigned long long*)o.bytes_dev;
+    v.stats = o.bytes_dev ? (unsigned long long*)o.stats_dev : nullptr;
+    v.defer_cap = o.defer_cap;
+    if (o.schedule > VR_SCHEDULE_HEAVIEST_FIRST) return fail(VR_E_INVALID, "unknown schedule");
+    return launch(s, algo, o.kernel, o.schedule, v, stream);
 }
+
+int vr_render_opts_init(vr_render_opts* opts) {
+    if (!opts) return fail(VR_E_INVALID, "NULL argument");
+    *opts = vr_render_opts{};
+    opts->struct_size = (uint32_t)sizeof(vr_render_opts);
+    opts->kernel = VR_KERNEL_AUTO;
+    opts->row_begin = 0;
+    opts->row_end = 0xFFFFFFFFu;
+    opts->band_rows = 0;
+    opts->rank = 0;
+    opts->nranks = 1;
+    opts->schedule = VR_SCHEDULE_AUTO;
+    return VR_OK;
+}
+
+namespace {
+vr_render_opts opts_rows(uint32_t row_begin, uint32_t row_end) {
+    vr_render_opts o;
+    vr_render_opts_init(&o);
+    o.row_begin = row_begin;
+    o.row_end = row_end;
+    return o;
+}
+}  // namespace
 
 int vr_render(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit, const float translation[3],
               uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin, uint32_t row_end, uint32_t* out_dev,
               void* stream) {
-    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, nullptr, 0, VR_SCHEDULE_AUTO};
+    const vr_render_opts o = opts_rows(row_begin, row_end);
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
@@ -1012,7 +1058,10 @@ int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t band_rows,
                     uint32_t rank, uint32_t nranks, uint32_t* out_dev, void* stream) {
     if (!band_rows) return fail(VR_E_INVALID, "band_rows must be > 0");
-    vr_render_opts o{VR_KERNEL_AUTO, 0, height, band_rows, rank, nranks, nullptr, 0, VR_SCHEDULE_AUTO};
+    vr_render_opts o = opts_rows(0, height);
+    o.band_rows = band_rows;
+    o.rank = rank;
+    o.nranks = nranks;
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 
@@ -1020,7 +1069,8 @@ int vr_render_count(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
                     const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t row_begin,
                     uint32_t row_end, uint32_t* out_dev, uint64_t* bytes_dev, void* stream) {
     if (!bytes_dev) return fail(VR_E_INVALID, "bytes_dev is NULL");
-    vr_render_opts o{VR_KERNEL_AUTO, row_begin, row_end, 0, 0, 1, bytes_dev, 0, VR_SCHEDULE_AUTO};
+    vr_render_opts o = opts_rows(row_begin, row_end);
+    o.bytes_dev = bytes_dev;
     return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
 }
 

@@ -89,7 +89,10 @@ struct KView {
     uint32_t band_minv;       // floor(2^32 / band_rows) (2^32 - 1 for 1): l / band_rows by a multiply-high
     uint32_t* out;
     unsigned long long* bytes;
-    uint32_t* defer;          // crawl deferral slot: [count, done, overflow, 0, records (kDeferRecWords each)...]
+    // (COUNT launches, optional) [0] crawl iterations the crawl pass fast-forwarded in
+    // closed form, [1] the existence-read bytes credited for them (part of *bytes, never loaded)
+    unsigned long long* stats;
+    uint32_t* defer;         // crawl deferral slot: [count, done, overflow, 0, records (kDeferRecWords each)...]
     uint32_t defer_cap;
     uint32_t crawl_rewalk;    // 1: deferred crawls are walked from the pixel's start (VR_KERNEL_TILE_REWALK)
     uint32_t crawl_rpw;       // crawl records per wave (0 = 4): 4 for a lone frame, 8 with frames in flight

@@ -603,7 +603,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                         crawl_after = this->iters + 8u;
                     } else {
                         this->iters += n;
-                        this->count(4u * n);
+                        this->count_ff(n);
                         inside = this->in_region_bits_nz(o);
                         if (!inside || this->iters >= kBudget) break;
                     }
@@ -1006,7 +1006,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                                 oL = ax3<PL>(on); oM = ax3<PM>(on); oS = ax3<PS>(on);
                                 gL = f2i(floorf(oL)); gM = f2i(floorf(oM)); gS = f2i(floorf(oS));
                                 it += n;
-                                this->count(4u * n);
+                                this->count_ff(n);
                             }
                         }
                     }
@@ -1396,9 +1396,10 @@ __device__ __forceinline__ uint32_t defer_rewalk(const KView& v, uint32_t x, uin
 // the oracle.
 template <int STORE, int ALGO, bool COUNT, bool CRAWL>
 __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint32_t x, uint32_t l,
-                                          uint32_t& bytes, uint32_t* iters = nullptr) {
+                                          uint32_t& bytes, uint32_t* iters = nullptr, uint32_t* ff = nullptr) {
     uint32_t col = 0;
     bytes = 0;
+    if (ff) *ff = 0;
     f3 ro, rd;
     if (pixel_ray<true>(v, x, l, ro, rd)) {
         Walker<STORE, COUNT, CRAWL> w(s, v);
@@ -1406,8 +1407,10 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
         if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
         if (iters) *iters = w.iters;              // the walk's length (the work order's cost)
         bytes = w.bytes + 4u;                     // + the pixel write
+        if (ff) *ff = w.ff;
         if (w.aborted) {
             col = 0;
+            if (ff) *ff = 0;
             if (Walker<STORE, COUNT, CRAWL>::kExact) {
                 bytes = 4u;
             } else {
@@ -1423,7 +1426,7 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
 // finished from there (its iterations and bytes so far are the record's).
 template <int STORE, int ALGO, bool COUNT>
 __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v,
-                                                 const uint32_t* r, uint32_t& bytes) {
+                                                 const uint32_t* r, uint32_t& bytes, uint32_t& ff) {
     const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
     Walker<STORE, COUNT, true> w(s, v);
     w.iters = r[9];
@@ -1444,9 +1447,11 @@ __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v
         col = r[18] * (uint32_t)!sh;
     }
     bytes = w.bytes + 4u;
+    ff = w.ff;
     if (w.aborted) {                              // never finishes (see shade)
         col = 0;
         bytes = 4u;
+        ff = 0;
     }
     return col;
 }
@@ -1454,6 +1459,14 @@ __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v
 __device__ __forceinline__ void add_bytes(const KView& v, uint32_t lane, unsigned long long b) {
     for (int off = 32; off > 0; off >>= 1) b += __shfl_down(b, off, 64);   // one atomic per wave
     if (lane == 0 && b) atomicAdd(v.bytes, b);
+}
+// the crawl pass's fast-forwarded iterations (KView::stats)
+__device__ __forceinline__ void add_ff(const KView& v, uint32_t lane, unsigned long long n) {
+    for (int off = 32; off > 0; off >>= 1) n += __shfl_down(n, off, 64);
+    if (lane == 0 && n && v.stats) {
+        atomicAdd(v.stats, n);
+        atomicAdd(v.stats + 1, 4ull * n);
+    }
 }
 
 // Tile pass: one lane per pixel, one wave per 8x8 tile, kTilesX x kTilesY tiles per workgroup.
@@ -1533,7 +1546,7 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && v.defer_stat) *v.defer_stat = total + overflow;
     if (total == 0u && overflow == 0u) return;   // nothing deferred (the usual case): no reset needed
     const uint32_t n = min(total, v.defer_cap);
-    unsigned long long bytes = 0;
+    unsigned long long bytes = 0, ffs = 0;
     // kCrawlRpw records per wave at a time (lanes 0 .. kCrawlRpw-1): each record is a long
     // chain of dependent iterations, and the lanes of a wave take different paths through
     // the walk, so fewer lanes per wave -- spread over more waves -- finish sooner
@@ -1566,21 +1579,27 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
                 r[15 + a] = (uint32_t)qa;
             }
         }
-        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b)
-                                         : shade_resume<STORE, ALGO, COUNT>(s, v, r, b);
+        uint32_t f = 0;
+        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f)
+                                         : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f);
         bytes += b;
+        ffs += f;
     }
     if (overflow != 0u) {
         // the list overflowed: the pixels the tile pass could not defer carry the marker
         const size_t npx = (size_t)v.local_rows * v.W;
         for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (size_t)gridDim.x * blockDim.x) {
             if (v.out[i] != kDeferMarker) continue;
-            uint32_t b;
-            v.out[i] = shade<STORE, ALGO, COUNT, true>(s, v, (uint32_t)(i % v.W), (uint32_t)(i / v.W), b);
+            uint32_t b, f = 0;
+            v.out[i] = shade<STORE, ALGO, COUNT, true>(s, v, (uint32_t)(i % v.W), (uint32_t)(i / v.W), b, nullptr, &f);
             bytes += b;
+            ffs += f;
         }
     }
-    if (COUNT) add_bytes(v, threadIdx.x & 63u, bytes);
+    if (COUNT) {
+        add_bytes(v, threadIdx.x & 63u, bytes);
+        add_ff(v, threadIdx.x & 63u, ffs);
+    }
     // Every workgroup has read the count (above) before it adds to `done`; the
     // last one clears the slot for its next launch (ordered by the kernel boundary).
     __syncthreads();

@@ -275,19 +275,29 @@ def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, 
               info: VoxelSceneInfo, width: int, height: int, out: torch.Tensor, row_begin: int = 0,
               row_end: int | None = None, band_rows: int = 0, rank: int = 0, nranks: int = 1,
               counter: torch.Tensor | None = None, kernel: Kernel = Kernel.AUTO, stream=None,
-              defer_cap: int = 0, schedule: Schedule = Schedule.AUTO) -> torch.Tensor:
+              defer_cap: int = 0, schedule: Schedule = Schedule.AUTO,
+              stats: torch.Tensor | None = None) -> torch.Tensor:
     """vr_render_ex: rows [row_begin,row_end), bands of band_rows (0 = one band) dealt to nranks ranks.
     defer_cap: capacity of the crawl pass's deferral list (0 = default; small values force its overflow path).
-    schedule: the tile pass's work order (Schedule)."""
+    schedule: the tile pass's work order (Schedule).
+    stats (with counter): CUDA int64[2], caller-zeroed: [0] crawl iterations fast-forwarded in closed form,
+    [1] the existence-read bytes credited for them (part of counter's count, never loaded)."""
     row_end = height if row_end is None else row_end
     rows = row_end - row_begin
     words = band_buffer_words(width, rows, band_rows or max(1, rows), nranks)
     _require_u32(out, words)
-    if counter is not None and (not counter.is_cuda or counter.dtype != torch.int64):
-        raise TypeError("counter must be a CUDA int64 tensor")
-    opts = _capi.VrRenderOpts(int(kernel), int(row_begin), int(row_end), int(band_rows), int(rank), int(nranks),
-                              c_void_p(counter.data_ptr()) if counter is not None else None, int(defer_cap),
-                              int(schedule))
+    for name, t in (("counter", counter), ("stats", stats)):
+        if t is not None and (not t.is_cuda or t.dtype != torch.int64):
+            raise TypeError(f"{name} must be a CUDA int64 tensor")
+    if stats is not None and (counter is None or stats.numel() < 2 or not stats.is_contiguous()):
+        raise ValueError("stats needs a counter and 2 contiguous int64 elements")
+    opts = _capi.VrRenderOpts()
+    check(lib().vr_render_opts_init(ctypes.byref(opts)), "vr_render_opts_init")
+    opts.kernel, opts.row_begin, opts.row_end = int(kernel), int(row_begin), int(row_end)
+    opts.band_rows, opts.rank, opts.nranks = int(band_rows), int(rank), int(nranks)
+    opts.bytes_dev = c_void_p(counter.data_ptr()) if counter is not None else None
+    opts.defer_cap, opts.schedule = int(defer_cap), int(schedule)
+    opts.stats_dev = c_void_p(stats.data_ptr()) if stats is not None else None
     check(lib().vr_render_ex(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
                              f3(info.translation), int(info.scale), int(width), int(height), ctypes.byref(opts),
                              c_void_p(out.data_ptr()), _stream_ptr(stream)), "vr_render_ex")

@@ -69,6 +69,31 @@ def pipeline_hw_queues(depth: int, nranks: int = 1) -> int:
     return 16 if streams > 4 else 0
 
 
+def init_frame_group(world: int, local_rank: int, backend: str = "auto", same_device: bool = False):
+    """The device and process group of one rank of the frame pipeline (bench.py's N > 1
+    path).  backend "auto"/"nccl": RCCL over xGMI, one GPU per rank (RCCL refuses two ranks
+    on one device).  "gloo": the same pipeline with the gather staged through host memory
+    (BandGather(stage_host=True)) -- what lets N ranks share one GPU (same_device: every
+    rank on cuda:0) to run the multi-rank path on a one-GPU box.
+    Returns (device, backend, stage_host); world == 1 starts no group."""
+    import torch.distributed as dist
+    dev_index = 0 if same_device else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    if backend == "auto":
+        backend = "nccl"
+    if backend not in ("nccl", "gloo"):
+        raise ValueError(f"unknown backend {backend!r}")
+    if same_device and world > 1 and backend == "nccl":
+        raise ValueError("several ranks on one GPU need the gloo backend (RCCL refuses a duplicate GPU)")
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    return dev, backend, backend == "gloo"
+
+
 def weak_scaled_resolution(width: int, height: int, nranks: int) -> tuple[int, int]:
     """The same view at about nranks x the pixels (both sides x sqrt(nranks), so the
     aspect ratio -- and with it Camera::Camera's view -- stays put and every rank
@@ -94,7 +119,7 @@ class BandGather:
     """
 
     def __init__(self, width: int, height: int, band_rows: int, rank: int, nranks: int,
-                 device, depth: int = 2, on_frame=None, rgb8: bool = False):
+                 device, depth: int = 2, on_frame=None, rgb8: bool = False, stage_host: bool = False):
         self.W, self.H, self.B = width, height, band_rows
         self.rank, self.R, self.depth = rank, nranks, depth
         words = band_buffer_words(width, height, band_rows, nranks)
@@ -110,6 +135,15 @@ class BandGather:
                        if self.rgb8 else None)
         self.recv = ([torch.empty((nranks, words * self.px), dtype=xdt, device=device) for _ in range(depth)]
                      if (rank == 0 and nranks > 1) else None)
+        # stage_host (a gloo group over GPU buffers -- gloo gathers host tensors only, e.g.
+        # several ranks sharing one GPU, where RCCL refuses): each frame's send buffer is
+        # copied to pinned host memory once its render is complete, gathered there, and the
+        # receive buffers are copied back to the device before the same assembly
+        self.stage = bool(stage_host) and nranks > 1 and torch.device(device).type == "cuda"
+        if self.stage:
+            self.h_send = [torch.empty(words * self.px, dtype=xdt, pin_memory=True) for _ in range(depth)]
+            self.h_recv = ([torch.empty((nranks, words * self.px), dtype=xdt, pin_memory=True) for _ in range(depth)]
+                           if rank == 0 else None)
         self.frame = (torch.empty((self.per * nranks * band_rows, width * self.px), dtype=xdt, device=device)
                       if rank == 0 else None)
         self.work = [None] * depth
@@ -124,6 +158,7 @@ class BandGather:
         self.pending = []            # slots in submission order
         self.on_frame = on_frame     # rank 0: callback(frame[:H]) after each assembled frame
         self.k = 0
+        self.last = 0                # the slot of the latest step
 
     def _slot_stream(self, slot: int):
         return torch.cuda.stream(self.streams[slot]) if self.streams is not None else contextlib.nullcontext()
@@ -144,6 +179,8 @@ class BandGather:
             else:
                 self.work[slot].wait()      # the slot's stream: bufs[slot] may be rendered into again
                 self.work[slot] = None
+                if self.stage and self.rank == 0:
+                    self.recv[slot].copy_(self.h_recv[slot], non_blocking=True)
                 if self.rank == 0:
                     if self.side is not None:
                         self.side.wait_stream(self.streams[slot])
@@ -176,9 +213,25 @@ class BandGather:
                 if self.copied[slot] is not None:       # its previous frame has left recv[slot]
                     torch.cuda.current_stream().wait_event(self.copied[slot])
                     self.copied[slot] = None
+                if self.stage:
+                    # (the host buffers are free: this slot's previous gather was waited on,
+                    # and on rank 0 its copy-back is ordered before this frame's copy-out)
+                    self.h_send[slot].copy_(send, non_blocking=True)
+                    torch.cuda.current_stream().synchronize()
+                    send = self.h_send[slot]
+                    dst = list(self.h_recv[slot].unbind(0)) if self.rank == 0 else None
                 self.work[slot] = dist.gather(send, dst, dst=0, async_op=True)
         self.pending.append(slot)
+        self.last = slot
         self.k += 1
+
+    def last_frame(self) -> torch.Tensor:
+        """After drain(): rank 0's last frame -- [H, W, 3] uint8 RGB8 when the bands travel
+        as RGB8, else [H, W] packed words (the band buffer itself with one rank)."""
+        if self.R == 1:
+            return self.bufs[self.last].view(-1, self.W)[:self.H]
+        f = self.frame[:self.H]
+        return f.view(self.H, self.W, 3) if self.rgb8 else f
 
     def drain(self) -> None:
         while self.pending:
