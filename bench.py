@@ -284,6 +284,10 @@ def main():
     # the untimed launches below make them); the pipelined loop's launches overlap on
     # BandGather's streams and run in grid order (include/vr.h vr_schedule).  The same
     # launches in grid order are timed too (kernel_ms_grid_order).
+    # One event pair brackets each phase of n_iso launches (an event pair around every
+    # launch adds ~10 us of event processing to each, profiles/r04/run1: 160.6 vs 150.8 us):
+    # kernel_ms = phase time / n_iso -- each launch's tile and crawl passes plus the
+    # dispatch gaps between back-to-back launches on one stream.
     n_iso = max(args.steps, 200)
     for _ in range(40):
         render(pipe.bufs[0])
@@ -292,13 +296,13 @@ def main():
         vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=BAND_ROWS, rank=rank, nranks=world,
                      stream=stream, schedule=vr.Schedule.GRID)
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_iso)]
-    ev_grid = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_iso)]
-    for evs, fn in ((ev_grid, render_grid), (ev, render)):
-        for a, b in evs:
-            a.record(stream)
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev_grid = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    for (a, b), fn in ((ev_grid, render_grid), (ev, render)):
+        a.record(stream)
+        for _ in range(n_iso):
             fn(pipe.bufs[0])
-            b.record(stream)
+        b.record(stream)
     torch.cuda.synchronize()
     # (the events are read after the timed loop: reading 200 of them takes ~17 ms,
     # long enough for an idle GPU to drop its clock before the timed loop starts)
@@ -321,33 +325,19 @@ def main():
             lat.append(time.perf_counter() - t0)
         frame_latency_ms = allreduce(float(np.median(lat)) * 1e3, op=dist.ReduceOp.MAX)
 
-    # the timed loop; each launch is also bracketed by HIP events on its own stream (the
-    # slot stream BandGather renders on): launch_ms_timed, the roofline's duration
-    ev_t = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    it_t = iter(ev_t)
-
-    def render_timed(buf):
-        a, b = next(it_t)
-        a.record()
-        render(buf)
-        b.record()
-
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        pipe.step(render_timed)
+        pipe.step(render)
     pipe.drain()
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
     dt = allreduce(dt, op=dist.ReduceOp.MAX)
     ms_per_step = dt / args.steps * 1e3
-    kern_all = [a.elapsed_time(b) for a, b in ev]
-    kern_ms = float(np.mean(kern_all))
-    kern_median = float(np.median(kern_all))
-    kern_grid_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_grid]))
-    launch_ms_timed = float(np.mean([a.elapsed_time(b) for a, b in ev_t]))
+    kern_ms = ev[0].elapsed_time(ev[1]) / n_iso
+    kern_grid_ms = ev_grid[0].elapsed_time(ev_grid[1]) / n_iso
     mrays = W * H / (ms_per_step * 1e-3) / 1e6
     if args.dump_frame and rank == 0:
         np.save(args.dump_frame, pipe.last_frame().cpu().numpy())
@@ -357,30 +347,34 @@ def main():
             return nbytes / (ms * 1e-3) / 1e9
         # The roofline's numerator: the bytes this launch's walks stand for minus
         # the existence reads of crawl iterations the crawl pass fast-forwards in closed form
-        # (it never issues them); its duration: the launch's own, timed in the timed loop.
-        achieved = gbs(issued_bytes, launch_ms_timed)
+        # (it never issues them).  Its duration: one launch on its own, in grid order -- a
+        # first render, as the reference's CLI makes (Main.cu:105-163), with no work order
+        # learned from earlier launches of the view.  (With frames in flight a launch's
+        # events also span the other frame's work, so no per-launch duration exists there;
+        # the pipelined rate is frac_pipelined.)
+        achieved = gbs(issued_bytes, kern_grid_ms)
         tj = load_traffic(args.traffic_json, cfg.name, world)
         traffic = tj.get("hbm_bytes_per_launch")
         roof = {"bound": None, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "achieved_basis": "algorithmic bytes issued per launch (SURVEY 8(d): the words the reference walk "
                                   "reads, counted by the instrumented kernel, minus the existence reads of crawl "
-                                  "iterations fast-forwarded in closed form) / the launch's mean duration in the "
-                                  "timed loop (launch_ms_timed: tile pass + crawl pass, HIP events on the launch's "
-                                  "stream) -- mostly served from L2/MALL, not HBM",
-                "launch_ms_timed": round(launch_ms_timed, 4),
+                                  "iterations fast-forwarded in closed form) / the mean duration of one launch "
+                                  "alone in grid order (kernel_ms_grid_order: tile pass + crawl pass, one HIP event "
+                                  "pair on the launch stream around the phase's back-to-back launches) -- mostly "
+                                  "served from L2/MALL, not HBM",
                 "algorithmic_bytes_per_launch": launch_bytes,
                 "algorithmic_bytes_issued_per_launch": issued_bytes,
                 "crawl_iterations_fast_forwarded": ff_iters,
                 "algorithmic_bytes_per_frame": frame_bytes, "algorithmic_bytes_issued_per_frame": frame_issued,
-                "frac_grid_order": round(gbs(issued_bytes, kern_grid_ms) / HBM_PEAK_GBS, 4),
                 "frac_learned_order": round(gbs(issued_bytes, kern_ms) / HBM_PEAK_GBS, 4),
                 "frac_pipelined": round(gbs(issued_bytes, ms_per_step) / HBM_PEAK_GBS, 4),
-                "frac_section8d": round(gbs(launch_bytes, launch_ms_timed) / HBM_PEAK_GBS, 4),
-                "fracs_basis": "the same issued bytes over: kernel_ms_grid_order (one launch alone in grid order, "
-                               "as a first render), kernel_ms (alone, heaviest tile groups first from an earlier "
-                               "launch's costs), ms_per_step (the pipelined frame rate); frac_section8d: the full "
-                               "SURVEY 8(d) count over launch_ms_timed",
+                "frac_section8d": round(gbs(launch_bytes, kern_grid_ms) / HBM_PEAK_GBS, 4),
+                "fracs_basis": "the same issued bytes over kernel_ms (one launch alone, heaviest tile groups first "
+                               "from an earlier launch's costs) and over ms_per_step (the pipelined frame rate); "
+                               "frac_section8d: the full SURVEY 8(d) count over kernel_ms_grid_order (crawl "
+                               "iterations credited as if loaded). profiles/roofline_phases.py recomputes frac and "
+                               "frac_learned_order from a rocprofv3 kernel trace of the same run",
                 }
         hbm_frac = valu_frac = None
         if traffic:
@@ -437,13 +431,12 @@ def main():
                        "voxels": int(len(rgb)), "parallelism": par, "frames_in_flight": pipe.depth,
                        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default")},
             "kernel_ms": round(kern_ms, 4),
-            "kernel_ms_median": round(kern_median, 4),
             "kernel_ms_grid_order": round(kern_grid_ms, 4),
-            "kernel_ms_basis": "one launch at a time on one stream (AUTO schedule: heaviest tile groups first, "
-                               "learned from earlier launches of the same view); kernel_ms_grid_order: the same "
-                               "launches in grid order (a first render); roofline.launch_ms_timed: the launches "
-                               "of the timed loop (frames in flight, grid order)",
-            "kernel_mrays_per_s": round(W * H / world / (kern_ms * 1e-3) / 1e6, 2),
+            "kernel_ms_basis": f"{n_iso} launches one after the other on one stream, one HIP event pair around them "
+                               "(each: tile pass + crawl pass): kernel_ms with the AUTO schedule (heaviest tile "
+                               "groups first, learned from earlier launches of the same view), kernel_ms_grid_order "
+                               "in grid order (a first render)",
+            "kernel_mrays_per_s": round(W * H / world / (kern_grid_ms * 1e-3) / 1e6, 2),
             "roofline": roof,
             # the non-instrumented launches of this run in order, per phase (a rocprofv3 kernel
             # trace of the same command splits into them: profiles/roofline_phases.py)

@@ -62,6 +62,8 @@ def lib() -> ctypes.CDLL:
         L.or_scene_min_coord.restype = c_int32
         L.or_scene_lookup.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32]
         L.or_scene_lookup.restype = c_uint32
+        L.or_scene_cuckoo_table.argtypes = [c_void_p, c_uint32, c_uint32, POINTER(c_int)]
+        L.or_scene_cuckoo_table.restype = c_int
         L.or_hash1.argtypes = [c_int32, c_uint32]
         L.or_hash1.restype = c_int32
         L.or_hash2.argtypes = [c_int32, c_uint32]
@@ -146,6 +148,14 @@ class Scene:
 
     def lookup(self, region, local) -> int:
         return lib().or_scene_lookup(self.h, *[int(v) for v in region], *[int(v) for v in local])
+
+    def cuckoo_table(self, region_index: int, key: int):
+        """(table 1 or 2 the key sits in -- 0 absent --, the region's table was rehashed)."""
+        rh = c_int()
+        t = lib().or_scene_cuckoo_table(self.h, int(region_index), int(key) & 0xFFFFFFFF, ctypes.byref(rh))
+        if t < 0:
+            raise ValueError("not a hashtable region")
+        return t, bool(rh.value)
 
     def render(self, algo: int, cam: OrCamera, lit: OrLighting, width: int, height: int, scale: int,
                translation=(0.0, 0.0, 0.0), row_begin: int = 0, row_end: int | None = None, nthreads: int = 0):

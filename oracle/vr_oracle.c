@@ -323,6 +323,21 @@ void or_scene_free(or_scene* s) {
     }
     free(s);
 }
+/* Test helper: the table (1 or 2) a key of region index r sits in, 0 if absent, -1 if
+ * r or the store is wrong; *rehashed = the region's table needed a rehash (prime or
+ * offset differ from the first attempt's). */
+int or_scene_cuckoo_table(const or_scene* s, uint32_t r, uint32_t key, int* rehashed) {
+    if (s->store != OR_STORE_HASHTABLE || r >= s->n_regions) return -1;
+    const or_cuckoo* t = &s->ht[r];
+    if (rehashed) *rehashed = t->prime != PRIME_TABLE[0] || t->offset != 0;
+    uint32_t M = t->M;
+    if (M == 0) return 0;
+    uint32_t k1 = ((uint32_t)or_hash1((int32_t)key, t->offset) % M + M) % M;
+    if (t->k1[k1] == key) return 1;
+    uint32_t k2 = ((uint32_t)or_hash2((int32_t)key, t->prime) % M + M) % M;
+    if (t->k2[k2] == key) return 2;
+    return 0;
+}
 uint32_t or_scene_diameter(const or_scene* s) { return s->D; }
 int32_t or_scene_min_coord(const or_scene* s) { return s->min_coord; }
 uint32_t or_scene_region_count(const or_scene* s) { return s->n_regions; }

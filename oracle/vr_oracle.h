@@ -73,6 +73,10 @@ uint32_t or_scene_region_count(const or_scene* s);
 uint32_t or_scene_lookup(const or_scene* s, int32_t rx, int32_t ry, int32_t rz,
                          int32_t x, int32_t y, int32_t z);
 
+/* Test helper: the cuckoo table (1, 2) key sits in within region index r (0 absent,
+ * -1 not a hashtable region); *rehashed = that region's table was rehashed. */
+int or_scene_cuckoo_table(const or_scene* s, uint32_t r, uint32_t key, int* rehashed);
+
 /* Diagnostic: an iteration budget per pixel for every later render
  * (process-global; UINT64_MAX = none, the default).  A pixel that exceeds it
  * renders as 0 with 4 bytes, like a walk that never finishes. */

@@ -12,11 +12,15 @@ dispatch (`crawl_kernel<S, A, false>`) on the same stream, sometimes plus a work
 Dispatch_Id order (submission order); the instrumented launch (`<..., true>`) is not counted.
 
 For each phase it writes `kernel_stats_<phase>.csv` (rocprofv3's kernel_stats.csv columns,
-over that phase's dispatches only) and reports the mean launch span (tile start -> crawl
-end: what the bench's HIP events bracket) and the fraction
-    algorithmic_bytes_issued_per_launch / span / 8 TB/s
-next to the bench's own figure for that phase: frac_grid_order (iso_grid), frac_learned_order
-(iso_learned) and frac (timed).  Results: <out_dir>/roofline_phases.json.
+over that phase's dispatches only) and reports
+  period  = (last dispatch end - first dispatch start) / launches: what bench.py's one HIP
+            event pair around the phase measures per launch (kernel_ms*),
+  kernels = the sum of the phase's per-kernel mean durations (tile + crawl + order builds
+            per launch): the kernel_stats figure, without the dispatch gaps,
+and the fraction algorithmic_bytes_issued_per_launch / duration / 8 TB/s for both, next
+to the bench's own figure for that phase: frac (iso_grid: one launch alone, grid order),
+frac_learned_order (iso_learned) and frac_pipelined (timed: per frame).
+Results: <out_dir>/roofline_phases.json.
 """
 from __future__ import annotations
 
@@ -93,16 +97,23 @@ def main():
             tot = sum(sum(v) for v in per.values())
             for name, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
                 w.writerow([name, len(v), sum(v), sum(v) / len(v), round(100.0 * sum(v) / tot, 2), min(v), max(v)])
-        span_ns = sum(spans) / len(spans)
+        first = min(t[3] for t, _, _ in part)
+        last = max(max([t[4]] + ([c[4]] if c else []) + [o[4] for o in od]) for t, c, od in part)
+        period_ns = (last - first) / n
+        kern_ns = sum(sum(v) for v in per.values()) / n
+        frac = lambda ns: round(issued / (ns * 1e-9) / 1e9 / PEAK_GBS, 4)  # noqa: E731
         res["phases"][ph] = {
             "launches": n,
-            "span_us": round(span_ns / 1e3, 3),
+            "period_us": round(period_ns / 1e3, 3),
+            "kernels_us": round(kern_ns / 1e3, 3),
+            "span_us": round(sum(spans) / len(spans) / 1e3, 3),
             "kernel_mean_us": {name: round(sum(v) / len(v) / 1e3, 3) for name, v in per.items()},
             "kernel_dispatches": {name: len(v) for name, v in per.items()},
-            "frac_from_trace": round(issued / (span_ns * 1e-9) / 1e9 / PEAK_GBS, 4),
+            "frac_from_trace": frac(period_ns),
+            "frac_from_kernel_means": frac(kern_ns),
         }
-    bench = {"iso_grid": roof.get("frac_grid_order"), "iso_learned": roof.get("frac_learned_order"),
-             "timed": roof.get("frac")}
+    bench = {"iso_grid": roof.get("frac"), "iso_learned": roof.get("frac_learned_order"),
+             "timed": roof.get("frac_pipelined")}
     for ph, fb in bench.items():
         if ph in res["phases"] and fb:
             p = res["phases"][ph]
@@ -112,7 +123,8 @@ def main():
         json.dump(res, f, indent=1)
     for ph, p in res["phases"].items():
         extra = f"  bench {p['frac_bench']:.4f} ({100 * p['rel_diff']:+.1f} %)" if "frac_bench" in p else ""
-        print(f"{ph:12s} {p['launches']:4d} launches  span {p['span_us']:9.3f} us  frac {p['frac_from_trace']:.4f}{extra}")
+        print(f"{ph:12s} {p['launches']:4d} launches  period {p['period_us']:9.3f} us  kernels {p['kernels_us']:9.3f} us  "
+              f"frac {p['frac_from_trace']:.4f} (kernel means {p['frac_from_kernel_means']:.4f}){extra}")
 
 
 if __name__ == "__main__":

@@ -11,6 +11,16 @@ sorted set of non-empty 8^3 clusters; lookups return the same values as
 VoxelClusterStore / CuckooHashTable (any correct structure does), and the VCS
 existence test is the cluster set (VoxelClusterStore.cuh:93-99).
 
+Algorithmic bytes, counted independently of the C oracle and the GPU
+counters: +4 per region-table read (Renderer.cuh:383,408,184,209,...); VCS: +4 per
+cluster-existence check (VoxelClusterStore.cuh:93-99; the duplicate directory read of
+lookupVoxel, :133, counted once), per lookup +4 for the block's count, +4 per key probe of
+performBinarySearch (:101-126, run here over the cluster's sorted keys) and +4 for the
+value on a match; cuckoo (CuckooHashTable.cuh:59-76): +4 key1, then +4 val1 on a match
+or +4 key2 (+4 val2 on a match) -- which table holds a key is the builder's placement,
+passed in (Scene(placement=...)); +4 per pixel write.  Iterations of a crawl run in
+closed form are credited +4 each (their existence reads).
+
 No iteration budget.  Walks that the reference never finishes (a loop
 iteration that leaves the loop's state unchanged repeats forever) render as
 0.  Cluster-skip crawls -- an axis pinned on its skip plane that EPSILON * d
@@ -182,7 +192,7 @@ def crawl_run(p, d, lo):
 
 
 class Scene:
-    def __init__(self, xyz, rgb, store: int):
+    def __init__(self, xyz, rgb, store: int, placement=None):
         """VoxelSceneCPU::insertVoxel (VoxelSceneCPU.cuh:16-46) over the voxels: region =
         floorf(x / 64.0f), local = ((x % 64) + 64) % 64, min/max region coordinate
         scalars starting at 0, later duplicates win (map assignment, :46)."""
@@ -203,6 +213,10 @@ class Scene:
         self.region_ids = np.unique(rid)
         cl = (rid << 9) | ((loc[:, 0] // 8) << 6) | ((loc[:, 1] // 8) << 3) | (loc[:, 2] // 8)
         self.clusters = np.unique(cl)
+        # placement(region_index, key) -> 1 or 2: the cuckoo table a stored key sits in
+        # (region_index = rank of the region among the occupied ones, the builders' order)
+        self.placement = placement
+        self._ckeys = {}
 
     def _rid_np(self, r):
         a = r - self.min
@@ -224,6 +238,22 @@ class Scene:
         i = np.searchsorted(self.keys, c)
         return int(self.vals[i]) if i < len(self.keys) and self.keys[i] == c else EMPTY
 
+    def region_index(self, rid):
+        return int(np.searchsorted(self.region_ids, rid))
+
+    def cluster_keys(self, rid, cid):
+        """The sorted keys and values of cluster cid of region rid: the block
+        [n, (k, v) x n] of VoxelClusterStore.cuh:61-76."""
+        got = self._ckeys.get((rid, cid))
+        if got is None:
+            a, b = np.searchsorted(self.keys, [rid << 32, (rid + 1) << 32])
+            k = (self.keys[a:b] & 0xFFFFFFFF).astype(np.int64)
+            c = ((k >> 23) << 6) | (((k >> 13) & 7) << 3) | ((k & 0x3FF) >> 3)
+            sel = c == cid
+            got = ([int(v) for v in k[sel]], [int(v) for v in self.vals[a:b][sel]])
+            self._ckeys[(rid, cid)] = got
+        return got
+
 
 class Lighting:
     def __init__(self, shadows=True, point=False, pos=(10.0, 10.0, -10.0)):
@@ -242,6 +272,7 @@ class Walk:
         self.lit = lit
         self.tr = V(*translation)
         self.iters = 0
+        self.bytes = 0
         self.aborted = False
 
     def tick(self):
@@ -255,17 +286,24 @@ class Walk:
         self.aborted = True
         return False
 
+    def crawled(self, n):
+        """n crawl iterations run in closed form: each one's existence read."""
+        self.iters += n
+        self.bytes += 4 * n
+
     # VoxelScene (Renderer.cuh:20-45)
     def in_scene(self, r):
         return all(u32(v - self.s.min) < self.s.D for v in r)
 
     def region(self, r):
+        self.bytes += 4                                  # getRegionStorageStructure's read
         return self.s.region_id(r)
 
     # StorageStructure adapters (StorageStructure.cuh:24-52)
     def exists(self, reg, x, y, z):
         if self.s.store == 1:
-            return True
+            return True                                  # HashTableStorageStructure: no read
+        self.bytes += 4                                  # the directory entry
         ux, uy, uz = u32(x), u32(y), u32(z)
         cid = (((ux // 8) << 6) | ((uy // 8) << 3) | (uz // 8)) & 0xFFFF
         if cid >= 0x8000 or cid >= 512:            # `short` id outside the directory
@@ -274,7 +312,29 @@ class Walk:
 
     def lookup(self, reg, x, y, z):
         key = u32((u32(x) << 20) | (u32(y) << 10) | u32(z))
-        return self.s.get(reg, key)
+        if self.s.store == 1:
+            # CuckooHashTable::lookupVoxel: key1 (+ val1), else key2 (+ val2)
+            col = self.s.get(reg, key)
+            table = self.s.placement(self.s.region_index(reg), key) if col != EMPTY else 0
+            self.bytes += 8 if table == 1 else (12 if table == 2 else 8)
+            return col
+        # performBinarySearch over the cluster's sorted keys (only after an existence
+        # check: the cluster is in the directory)
+        cid = (((u32(x) // 8) << 6) | ((u32(y) // 8) << 3) | (u32(z) // 8)) & 0xFFFF
+        keys, vals = self.s.cluster_keys(reg, cid)
+        self.bytes += 4                                  # the block's count
+        low, high = 0, len(keys) - 1
+        while low <= high:
+            mid = low + (high - low) // 2
+            self.bytes += 4                              # key probe
+            if keys[mid] == key:
+                self.bytes += 4                          # value
+                return vals[mid]
+            if keys[mid] < key:
+                low = mid + 1
+            else:
+                high = mid - 1
+        return EMPTY
 
     # lighting (Renderer.cuh:57-86, 249-258; VoxelFunctions.cuh:69-83)
     @staticmethod
@@ -362,7 +422,7 @@ class Walk:
                     if n is None:
                         self.forever()
                         return EMPTY
-                    self.iters += n
+                    self.crawled(n)
                 continue
             col = self.lookup(reg, vx, vy, vz)
             if col != EMPTY:
@@ -474,7 +534,7 @@ class Walk:
                     if n is None:
                         self.forever()
                         return EMPTY
-                    self.iters += n
+                    self.crawled(n)
                     for i in range(3):
                         g[i] = f2i(np.floor(st["old"][i]))
             col = self.lookup(reg, *g)
@@ -614,9 +674,12 @@ def camera(eye, at, up, fov, aspect):
     return o, llc, u.scale(F(2) * hw), v.scale(F(2) * hh)
 
 
-def render_pixel(scene, lit, cam_fields, W, H, x, y, scale, longest, translation=(0.0, 0.0, 0.0), iters=False):
+def render_pixel(scene, lit, cam_fields, W, H, x, y, scale, longest, translation=(0.0, 0.0, 0.0), iters=False,
+                 nbytes=False):
     """calculateWorldRay + kernel body (Renderer.cuh:1013-1063). cam_fields: (origin, llc, hor, ver) V's.
-    iters: return (colour, loop iterations of the pixel, crawl iterations included)."""
+    iters: return (colour, loop iterations of the pixel, crawl iterations included);
+    nbytes: return (colour, algorithmic bytes of the pixel: its walks' reads + the 4-B pixel write;
+    4 alone for a walk that never finishes)."""
     org, llc, hor, ver = cam_fields
     u = (F(x) + F(0.5)) / F(W)
     v = (F(u32(H - y)) + F(0.5)) / F(H)
@@ -625,4 +688,6 @@ def render_pixel(scene, lit, cam_fields, W, H, x, y, scale, longest, translation
     w = Walk(scene, lit, translation)
     col = w.scene(ro, rd, scale, longest)
     col = 0 if w.aborted else col
+    if nbytes:
+        return col, (4 if w.aborted else w.bytes + 4)
     return (col, w.iters) if iters else col

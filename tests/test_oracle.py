@@ -231,11 +231,36 @@ def test_c5_crawl_pixels_python_restatement():
             col, its = pyref.render_pixel(ps, pyref.Lighting(), pc, W, H, p["x"], p["y"], cfg.scale, algo == 0,
                                           iters=True)
             assert (col, its) == (p["colour"], p["iterations"]), (p, col, its)
+            _, nb = pyref.render_pixel(ps, pyref.Lighting(), pc, W, H, p["x"], p["y"], cfg.scale, algo == 0,
+                                       nbytes=True)
+            assert nb == p["bytes"], (p, nb)
+
+
+def _pyref_scene(sc, xyz, rgb, store):
+    """The Python restatement of the same voxels; a cuckoo store takes the oracle build's
+    placement (which table a key sits in) -- the only input the byte rule needs from a
+    builder (CuckooHashTable.cuh:59-76: a key in table 2 costs key1 + key2 + val2)."""
+    return pyref.Scene(xyz, rgb, store, placement=(lambda r, k: sc.cuckoo_table(r, k)[0]) if store == 1 else None)
+
+
+def _rays_agree(sc, ps, algo, cam, lit, plit, W, H, scale, px, py, translation=(0.0, 0.0, 0.0), where=""):
+    """Colour AND SURVEY 8(d) bytes of every ray: the C oracle vs the Python restatement."""
+    got, b = sc.render_pixels(algo, cam, lit, W, H, scale, px, py, translation=translation)
+    pc = _pyref_camera(cam)
+    hits = 0
+    for i in range(len(px)):
+        col, nb = pyref.render_pixel(ps, plit, pc, W, H, int(px[i]), int(py[i]), scale,
+                                     algo == oracle.ALGO_LONGESTAXIS, translation=translation, nbytes=True)
+        assert (int(got[i]), int(b[i])) == (col, nb), (where, algo, int(px[i]), int(py[i]), hex(int(got[i])), hex(col),
+                                                       int(b[i]), nb)
+        hits += col != 0
+    return hits
 
 
 @pytest.mark.parametrize("algo", [oracle.ALGO_ORIGINAL, oracle.ALGO_LONGESTAXIS])
 def test_c2_c3_rays_python_restatement(algo):
-    """120 sampled rays of the C2 (original) / C3 (longest axis) 1920x1080 frame, both stores."""
+    """120 sampled rays of the C2 (original) / C3 (longest axis) 1920x1080 frame, both stores:
+    colours and per-ray algorithmic bytes equal."""
     cfg, (xyz, rgb) = _cfg_scene("C2")
     W, H = cfg.width, cfg.height
     cam, lit = oracle.reference_camera(W, H), oracle.lighting()
@@ -244,21 +269,60 @@ def test_c2_c3_rays_python_restatement(algo):
     py = rng.integers(0, H, 120).astype(np.uint32)
     for store in (0, 1):
         sc = oracle.Scene(xyz, rgb, store)
-        ps = pyref.Scene(xyz, rgb, store)
-        got, _ = sc.render_pixels(algo, cam, lit, W, H, cfg.scale, px, py)
-        hits = 0
-        for i in range(len(px)):
-            want = pyref.render_pixel(ps, pyref.Lighting(), _pyref_camera(cam), W, H, int(px[i]), int(py[i]),
-                                      cfg.scale, algo == 0)
-            assert int(got[i]) == want, (store, int(px[i]), int(py[i]))
-            hits += want != 0
-        assert hits > 20
+        ps = _pyref_scene(sc, xyz, rgb, store)
+        assert _rays_agree(sc, ps, algo, cam, lit, pyref.Lighting(), W, H, cfg.scale, px, py, where=store) > 20
+
+
+def test_c4_rays_bytes_python_restatement():
+    """>= 100 rays of the C4 frame (512^3 dense cuckoo store, 20 M voxels, hashtable +
+    original): colours and per-ray bytes, the Python restatement's cuckoo byte rule over
+    the oracle build's placement."""
+    cfg, (xyz, rgb) = _cfg_scene("C4")
+    W, H = cfg.width, cfg.height
+    sc = oracle.Scene(xyz, rgb, 1)
+    ps = _pyref_scene(sc, xyz, rgb, 1)
+    del xyz, rgb
+    cam, lit = oracle.reference_camera(W, H), oracle.lighting()
+    rng = np.random.default_rng(44)
+    px = rng.integers(0, W, 110).astype(np.uint32)
+    py = rng.integers(0, H, 110).astype(np.uint32)
+    assert _rays_agree(sc, ps, oracle.ALGO_ORIGINAL, cam, lit, pyref.Lighting(), W, H, cfg.scale, px, py) > 40
+
+
+def test_rehashed_cuckoo_region_bytes_python_restatement():
+    """A cuckoo region whose build needs a rehash (8 keys that share both default hash
+    slots: the eviction chain passes createCuckooHashTable's limit, CuckooHashTable.cuh:
+    112-123, and a new prime/offset is drawn) beside a dense block in the next region:
+    every pixel of a 48x40 frame from two views, both algorithms, agrees in colour and
+    bytes -- lookups into table 2 cost 4 B more -- and rays do hit the rehashed keys."""
+    keys = [(0, 15, 63), (0, 36, 33), (0, 57, 6), (0, 60, 63), (3, 3, 45), (3, 12, 57), (3, 15, 48), (3, 45, 9)]
+    g = np.stack(np.meshgrid(np.arange(64, 72), np.arange(0, 20), np.arange(20, 44), indexing="ij"), -1).reshape(-1, 3)
+    xyz = np.concatenate([np.array(keys), g]).astype(np.int32)
+    rgb = (np.arange(len(xyz), dtype=np.uint32) * 2654435761 % (1 << 24)).astype(np.uint32)
+    sc = oracle.Scene(xyz, rgb, 1)
+    assert sc.cuckoo_table(0, 0)[1], "region 0 is expected to need a rehash"
+    tables = [sc.cuckoo_table(0, (x << 20) | (y << 10) | z)[0] for x, y, z in keys]
+    assert set(tables) == {1, 2}
+    ps = _pyref_scene(sc, xyz, rgb, 1)
+    W, H = 48, 40
+    px, py = np.meshgrid(np.arange(W, dtype=np.uint32), np.arange(H, dtype=np.uint32))
+    px, py = px.reshape(-1), py.reshape(-1)
+    hit_keys = 0
+    for eye, at in (((-3.0, 40.0, 30.0), (4.0, 32.0, 30.0)), ((40.0, 70.0, 80.0), (2.0, 30.0, 30.0))):
+        cam = oracle.camera(eye, at, (0.0, 1.0, 0.0), 70.0, W / H)
+        for algo in (oracle.ALGO_ORIGINAL, oracle.ALGO_LONGESTAXIS):
+            _rays_agree(sc, ps, algo, cam, oracle.lighting(use_shadows=False), pyref.Lighting(shadows=False), W, H, 1,
+                        px, py, where=eye)
+            img, _ = sc.render(algo, cam, oracle.lighting(use_shadows=False), W, H, 1)
+            hit_keys += int(np.count_nonzero(img != 0))
+    assert hit_keys > 0
 
 
 def test_alias_rays_python_restatement():
     """Rays that probe outside their region where the `short` cluster id aliases into
     the directory (tests/golden/alias_rays.json): the oracle reproduces the committed
-    frames, reports the aliased probes, and the Python restatement agrees on every pixel."""
+    frames, reports the aliased probes, and the Python restatement agrees on every pixel
+    and on each frame's algorithmic bytes."""
     fx = json.load(open(os.path.join(GOLDEN, "alias_rays.json")))
     d = np.load(os.path.join(GOLDEN, fx["scene"]))
     sc = oracle.Scene(d["xyz"], d["rgb"], 0)
@@ -274,9 +338,13 @@ def test_alias_rays_python_restatement():
         al = np.flatnonzero(st[..., 8].sum(-1).reshape(-1))
         assert al.tolist() == c["alias_pixels"]
         n_alias += len(al)
+        total = 0
         for i in range(W * H):
-            want = pyref.render_pixel(ps, pyref.Lighting(), _pyref_camera(cam), W, H, i % W, i // W, 1, True)
+            want, nb = pyref.render_pixel(ps, pyref.Lighting(), _pyref_camera(cam), W, H, i % W, i // W, 1, True,
+                                          nbytes=True)
             assert want == c["pixels"][i], (c["eye"], i)
+            total += nb
+        assert total == c["algorithmic_bytes"], c["eye"]       # the aliasing slow path's bytes too
     assert n_alias >= 100
 
 
@@ -353,10 +421,7 @@ def test_fuzz_cases_python_restatement(seed):
     pc = _pyref_camera(cam)
     for store in (oracle.STORE_VCS, oracle.STORE_HASHTABLE):
         sc = oracle.Scene(c.xyz, c.rgb, store)
-        ps = pyref.Scene(c.xyz, c.rgb, store)
+        ps = _pyref_scene(sc, c.xyz, c.rgb, store)
         for algo in (oracle.ALGO_ORIGINAL, oracle.ALGO_LONGESTAXIS):
-            got, _ = sc.render_pixels(algo, cam, lit, c.W, c.H, c.scale, px, py, translation=c.translation)
-            for i in range(len(px)):
-                want = pyref.render_pixel(ps, plit, pc, c.W, c.H, int(px[i]), int(py[i]), c.scale,
-                                          algo == oracle.ALGO_LONGESTAXIS, translation=c.translation)
-                assert int(got[i]) == want, (seed, store, algo, int(px[i]), int(py[i]), hex(int(got[i])), hex(want))
+            _rays_agree(sc, ps, algo, cam, lit, plit, c.W, c.H, c.scale, px, py, translation=c.translation,
+                        where=(seed, store))

@@ -186,6 +186,9 @@ struct Ctx {
     bool aborted = false;
     uint32_t bytes = 0;
     uint32_t ff = 0;     // (COUNT) crawl iterations credited in closed form (crawl_run)
+#ifdef VR_DIAG
+    uint32_t d_runs = 0, d_trips = 0;   // (diagnostic builds) crawl_run calls that applied steps, their loop trips
+#endif
 
     __device__ Ctx(const KScene& s_, const KView& v_) : s(s_), v(v_) {}
 
@@ -195,6 +198,10 @@ struct Ctx {
     // n crawl iterations fast-forwarded: the existence read each of them stands for
     //  is credited, but the kernel never issues it
     __device__ __forceinline__ void count_ff(uint32_t n) {
+#ifdef VR_DIAG
+        ++d_runs;
+        ff += COUNT ? 0u : n;
+#endif
         if (COUNT) {
             bytes += 4u * n;
             ff += n;

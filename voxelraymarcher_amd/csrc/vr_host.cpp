@@ -138,8 +138,9 @@ struct vr_scene {
     uint32_t n_regions = 0;
     uint64_t n_voxels = 0;
     DevBuf region_slot, vcs_mask, vcs_vals, ht_meta, ht_slots;
+    DevBuf vcs_cbits;   // derived (not part of vr_scene_digest): cluster-existence bits per region
     uint64_t device_bytes() const {
-        return region_slot.bytes + vcs_mask.bytes + vcs_vals.bytes + ht_meta.bytes + ht_slots.bytes;
+        return region_slot.bytes + vcs_mask.bytes + vcs_vals.bytes + ht_meta.bytes + ht_slots.bytes + vcs_cbits.bytes;
     }
 };
 
@@ -159,7 +160,7 @@ struct DeviceGuard {
 
 void free_scene(vr_scene* s) {
     if (!s) return;
-    DevBuf* bufs[] = {&s->region_slot, &s->vcs_mask, &s->vcs_vals, &s->ht_meta, &s->ht_slots};
+    DevBuf* bufs[] = {&s->region_slot, &s->vcs_mask, &s->vcs_vals, &s->ht_meta, &s->ht_slots, &s->vcs_cbits};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     delete s;
@@ -379,8 +380,45 @@ int build_scene_device(int device, vr_store store, const int32_t* xyz, const uin
     return VR_OK;
 }
 
+// The derived per-region cluster-existence bits of a VCS scene (vr_internal.h KScene),
+// made on the device from the mask records either builder wrote.
+int add_cluster_bits(vr_scene* s, hipStream_t stream) {
+    if (s->store != VR_STORE_VCS) return VR_OK;
+    DeviceGuard dg(s->device);
+    const uint32_t nr = std::max(1u, s->n_regions);
+    const size_t bytes = (size_t)nr * 16u * sizeof(uint32_t);
+    hipError_t e = hipMalloc(&s->vcs_cbits.p, bytes);
+    if (e != hipSuccess) {
+        s->vcs_cbits.p = nullptr;
+        return hip_fail(e, "hipMalloc(cluster bits)");
+    }
+    s->vcs_cbits.bytes = bytes;
+    e = hipMemsetAsync(s->vcs_cbits.p, 0, bytes, stream);
+    if (e == hipSuccess && s->n_regions)
+        e = vr::launch_cluster_bits((const uint2*)s->vcs_mask.p, s->n_regions, (uint32_t*)s->vcs_cbits.p, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hip_fail(e, "cluster bits");
+    return VR_OK;
+}
+
+int build_scene_raw(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, bool on_device,
+                    vr_build mode, void* stream, vr_scene** out);
+
 int build_scene(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, bool on_device,
                 vr_build mode, void* stream, vr_scene** out) {
+    int rc = build_scene_raw(device, store, xyz, rgb, n, on_device, mode, stream, out);
+    if (rc) return rc;
+    rc = add_cluster_bits(*out, (hipStream_t)stream);
+    if (rc) {
+        DeviceGuard dg((*out)->device);
+        free_scene(*out);
+        *out = nullptr;
+    }
+    return rc;
+}
+
+int build_scene_raw(int device, vr_store store, const int32_t* xyz, const uint32_t* rgb, size_t n, bool on_device,
+                    vr_build mode, void* stream, vr_scene** out) {
     if (!out) return fail(VR_E_INVALID, "out is NULL");
     *out = nullptr;
     if (store != VR_STORE_VCS && store != VR_STORE_HASHTABLE) return fail(VR_E_INVALID, "unknown store");
@@ -410,6 +448,7 @@ vr::KScene kscene(const vr_scene* s) {
     k.region_slot = (const uint32_t*)s->region_slot.p;
     k.vcs_mask = (const uint2*)s->vcs_mask.p;
     k.vcs_vals = (const uint32_t*)s->vcs_vals.p;
+    k.vcs_cbits = (const uint32_t*)s->vcs_cbits.p;
     k.ht_meta = (const uint4*)s->ht_meta.p;
     k.ht_slots = (const uint2*)s->ht_slots.p;
     k.D = s->D;

@@ -52,10 +52,14 @@ constexpr uint32_t kVcsMaxRegions = 65536u;
 //  Cuckoo: ht_meta[r]        : {base, M, prime, offset}
 //          ht_slots[base+i]  : table 1 slot i {key, value};
 //          ht_slots[base+M+i]: table 2 slot i {key, value}; empty key = kEmpty
+//  VCS   : vcs_cbits[r*16 + w]: bit b set <=> cluster slot 32w+b of region r is present
+//                              (derived from vcs_mask after either build; the crawl
+//                              pass caches a region's 64 B in LDS)
 struct KScene {
     const uint32_t* region_slot;
     const uint2* vcs_mask;
     const uint32_t* vcs_vals;
+    const uint32_t* vcs_cbits;
     const uint4* ht_meta;
     const uint2* ht_slots;
     uint32_t D;
@@ -130,6 +134,8 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
                         hipStream_t stream, uint32_t crawl_wgs);
 // Crawl-pass grid for a launch that expects about `records` deferred pixels.
 uint32_t crawl_grid(uint32_t records, uint32_t rpw);
+// vcs_cbits of a VCS scene from its mask records (one thread per 32 cluster slots).
+hipError_t launch_cluster_bits(const uint2* vcs_mask, uint32_t n_regions, uint32_t* cbits, hipStream_t stream);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);
 // The tile pass's grid for a view (columns, rows of workgroups) and its waves per workgroup.
 void march_grid(const KView& v, uint32_t& columns, uint32_t& rows);

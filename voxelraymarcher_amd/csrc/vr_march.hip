@@ -24,6 +24,9 @@
 // active lane.  Never part of the library build.
 #ifdef VR_DIAG
 __device__ unsigned long long g_vr_diag[32];
+// per crawl record of the last crawl pass: {shader cycles, plain loop iterations, crawl_run
+// calls that applied steps, their loop trips} (profiles/crawl_prof.py)
+__device__ unsigned int g_vr_crawl_prof[16384 * 4];
 #define VR_DIAG_COUNT(k)                                                              \
     do {                                                                             \
         if (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) \
@@ -120,7 +123,7 @@ __device__ __forceinline__ Crawl crawl_steps(f3 on, f3 d, int32_t vx, int32_t vy
 // crawl of 10^5..10^6 iterations costs a few dozen loop trips instead of as many
 // dependent mask loads.
 __device__ __forceinline__ uint32_t crawl_run(f3& o, f3 d, int32_t qx, int32_t qy, int32_t qz, bool px, bool py,
-                                              bool pz, uint32_t room) {
+                                              bool pz, uint32_t room, uint32_t* trips = nullptr) {
     const f3 c{kEps * d.x, kEps * d.y, kEps * d.z};
     const int32_t lx = qx & ~7, ly = qy & ~7, lz = qz & ~7;
     // an axis pinned on its cluster plane: direction negative, on the plane, unmoved by its step
@@ -136,6 +139,7 @@ __device__ __forceinline__ uint32_t crawl_run(f3& o, f3 d, int32_t qx, int32_t q
     uint32_t n = 0;
 #pragma unroll 1
     for (uint32_t trip = 0; trip < 4096u && n < room; ++trip) {
+        if (trips) ++*trips;
         const Crawl cw = crawl_steps(o, d, qx, qy, qz, px, py, pz, room - n);
         if (cw.m != 0u) {
             const float fm = (float)cw.m;       // exact: m * delta_i stays inside the binade
@@ -268,6 +272,13 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
     // what a deferred crawl must know to be resumed (see the deferral below):
     // bit 1 = the shadow walk is the longest-axis one; the lit colour of the hit
     uint32_t ctx = 0, lit_saved = 0;
+    // Crawl pass (VCS): this lane's LDS copy of the cluster-existence bits of region
+    // bm_reg (KScene::vcs_cbits, 16 words), or null.  A crawl record's remaining walk
+    // -- up to ~280 iterations, mostly cluster skips through C5's empty clusters, each
+    // a dependent mask load from MALL/HBM -- then loads a mask word only in present
+    // clusters: a skip step reads one LDS word instead.
+    uint32_t* lbm = nullptr;
+    uint32_t bm_reg = kNone;
 
     // rayMarchVoxelGrid (Renderer.cuh:260-336) and, SHADOW, shadowRayMarchVoxelGrid (:100-172).
     // The cluster-skip step (:290-306) and the voxel step (:318-331) share one
@@ -343,6 +354,13 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             // the region's mask words as a 32-bit byte offset from the scene's (uniform)
             // mask array: the loads take the SGPR-base form (one VGPR, no 64-bit add)
             const uint32_t moff = reg << 16;
+            if (CRAWL && lbm && reg != bm_reg) {      // the region's cluster-existence bits into LDS
+                const uint4* src = reinterpret_cast<const uint4*>(s.vcs_cbits + (size_t)reg * 16u);
+                const uint4 b0 = src[0], b1 = src[1], b2 = src[2], b3 = src[3];
+                uint4* dst = reinterpret_cast<uint4*>(lbm);
+                dst[0] = b0; dst[1] = b1; dst[2] = b2; dst[3] = b3;
+                bm_reg = reg;
+            }
             // Straight-line body with one exit: the hit test, the region test of
             // the stepped position and the iteration budget are folded into a
             // single condition; the step of the hit iteration is computed and
@@ -416,8 +434,17 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                             const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
                             this->count(4);
                             const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
-                            blk = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) +
-                                                                  (moff | (wi << 3)));
+                            if constexpr (CRAWL) {
+                                // (crawl pass) cluster slot wi >> 4 absent per the LDS bits: no load
+                                const bool pres = !lbm || ((lbm[wi >> 9] >> ((wi >> 4) & 31u)) & 1u);
+                                blk = Blk{0u, kNone};
+                                if (pres)
+                                    blk = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) +
+                                                                          (moff | (wi << 3)));
+                            } else {
+                                blk = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) +
+                                                                      (moff | (wi << 3)));
+                            }
                             __builtin_amdgcn_sched_barrier(0);   // issue the load before the planes
                             // both candidate planes, computed while the mask word is in
                             // flight and materialised (with the whole 8-B word: one load)
@@ -596,7 +623,11 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                 } else {
                     // Off the hot loop: fast-forward the identical crawl iterations
                     // exactly, then resume the walk (no region-entry step).
+#ifdef VR_DIAG
+                    const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters, &this->d_trips);
+#else
                     const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters);
+#endif
                     // none (not a real crawl, or its next step leaves the cluster): a few plain
                     // iterations, then re-arm
                     if (n == 0u) {
@@ -1001,7 +1032,11 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                             const f3 dd = to_f3(dL, dM, dS);
                             const i3 q = to_i3(qL, qM, qS);
                             const uint32_t n = crawl_run(on, dd, q.x, q.y, q.z, dd.x > 0.0f, dd.y > 0.0f, dd.z > 0.0f,
-                                                         kBudget - it);
+                                                         kBudget - it
+#ifdef VR_DIAG
+                                                         , &this->d_trips
+#endif
+                                                         );
                             if (n != 0u) {
                                 oL = ax3<PL>(on); oM = ax3<PM>(on); oS = ax3<PS>(on);
                                 gL = f2i(floorf(oL)); gM = f2i(floorf(oM)); gS = f2i(floorf(oS));
@@ -1396,18 +1431,23 @@ __device__ __forceinline__ uint32_t defer_rewalk(const KView& v, uint32_t x, uin
 // the oracle.
 template <int STORE, int ALGO, bool COUNT, bool CRAWL>
 __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint32_t x, uint32_t l,
-                                          uint32_t& bytes, uint32_t* iters = nullptr, uint32_t* ff = nullptr) {
+                                          uint32_t& bytes, uint32_t* iters = nullptr, uint32_t* ff = nullptr,
+                                          uint32_t* dg = nullptr, uint32_t* lbm = nullptr) {
     uint32_t col = 0;
     bytes = 0;
     if (ff) *ff = 0;
     f3 ro, rd;
     if (pixel_ray<true>(v, x, l, ro, rd)) {
         Walker<STORE, COUNT, CRAWL> w(s, v);
+        w.lbm = lbm;
         Hit h;
         if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
         if (iters) *iters = w.iters;              // the walk's length (the work order's cost)
         bytes = w.bytes + 4u;                     // + the pixel write
         if (ff) *ff = w.ff;
+#ifdef VR_DIAG
+        if (dg) { dg[0] = w.iters - w.ff; dg[1] = w.d_runs; dg[2] = w.d_trips; }
+#endif
         if (w.aborted) {
             col = 0;
             if (ff) *ff = 0;
@@ -1426,9 +1466,11 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
 // finished from there (its iterations and bytes so far are the record's).
 template <int STORE, int ALGO, bool COUNT>
 __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v,
-                                                 const uint32_t* r, uint32_t& bytes, uint32_t& ff) {
+                                                 const uint32_t* r, uint32_t& bytes, uint32_t& ff,
+                                                 uint32_t* dg = nullptr, uint32_t* lbm = nullptr) {
     const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
     Walker<STORE, COUNT, true> w(s, v);
+    w.lbm = lbm;
     w.iters = r[9];
     w.bytes = r[10];
     const f3 o{__uint_as_float(r[2]), __uint_as_float(r[3]), __uint_as_float(r[4])};
@@ -1448,6 +1490,9 @@ __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v
     }
     bytes = w.bytes + 4u;
     ff = w.ff;
+#ifdef VR_DIAG
+    if (dg) { dg[0] = w.iters - r[9] - w.ff; dg[1] = w.d_runs; dg[2] = w.d_trips; }
+#endif
     if (w.aborted) {                              // never finishes (see shade)
         col = 0;
         bytes = 4u;
@@ -1533,9 +1578,12 @@ __global__ __launch_bounds__(1024) void order_kernel(const uint32_t* __restrict_
 #define VR_CRAWL_RPW 4
 #endif
 constexpr uint32_t kCrawlRpw = VR_CRAWL_RPW;
+constexpr uint32_t kCrawlMaxRpw = 16;     // records per wave with an LDS bitmap slot
 template <int STORE, int ALGO, bool COUNT>
 __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     __shared__ uint32_t n_lds, ovf_lds;
+    // per record lane: the cluster-existence bits of the region its walk is in (VCS)
+    __shared__ __attribute__((aligned(16))) uint32_t lbm_all[(256 / 64) * kCrawlMaxRpw * 16];
     if (threadIdx.x == 0) {
         n_lds = v.defer[0];
         ovf_lds = v.defer[2];
@@ -1556,6 +1604,9 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     const uint32_t rpw = v.crawl_rpw ? v.crawl_rpw : kCrawlRpw;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, wlane = threadIdx.x & 63u;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    uint32_t* lbm = (STORE == STORE_VCS && s.vcs_cbits && rpw <= kCrawlMaxRpw && wlane < rpw)
+                        ? lbm_all + ((threadIdx.x >> 6) * kCrawlMaxRpw + wlane) * 16u
+                        : nullptr;
     for (uint32_t i = wave * rpw + wlane; wlane < rpw && i < n; i += nwaves * rpw) {
         uint32_t* r = v.defer + 4 + (size_t)i * kDeferRecWords;
         uint32_t b;
@@ -1580,8 +1631,22 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
             }
         }
         uint32_t f = 0;
-        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f)
-                                         : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f);
+#ifdef VR_DIAG
+        uint32_t dg[3] = {0, 0, 0};
+        const long long c0 = clock64();
+        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, dg, lbm)
+                                         : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f, dg, lbm);
+        const long long c1 = clock64();
+        if (i < 16384u) {
+            g_vr_crawl_prof[4 * i + 0] = (uint32_t)min(c1 - c0, 0xFFFFFFFFll);
+            g_vr_crawl_prof[4 * i + 1] = dg[0] | (amb ? 0x80000000u : 0u);
+            g_vr_crawl_prof[4 * i + 2] = dg[1];
+            g_vr_crawl_prof[4 * i + 3] = dg[2];
+        }
+#else
+        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, nullptr, lbm)
+                                         : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f, nullptr, lbm);
+#endif
         bytes += b;
         ffs += f;
     }
@@ -1608,6 +1673,17 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
         v.defer[1] = 0;
         v.defer[2] = 0;
     }
+}
+
+// KScene::vcs_cbits: thread (r, w) ORs the existence of cluster slots 32w..32w+31 of
+// region r (a present cluster's record has an index in every word, vr_internal.h)
+__global__ void cluster_bits_kernel(const uint2* __restrict__ mask, uint32_t n_regions, uint32_t* __restrict__ cbits) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_regions * 16u) return;
+    const uint2* m = mask + (size_t)(t >> 4) * 8192u + (size_t)(t & 15u) * 32u * 16u;
+    uint32_t b = 0;
+    for (uint32_t k = 0; k < 32u; ++k) b |= (m[k * 16u].y != kNone ? 1u : 0u) << k;
+    cbits[t] = b;
 }
 
 __global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __restrict__ rgb, uint64_t n) {
@@ -1689,6 +1765,14 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
     return hipGetLastError();
 }
 
+hipError_t launch_cluster_bits(const uint2* vcs_mask, uint32_t n_regions, uint32_t* cbits, hipStream_t stream) {
+    if (n_regions == 0) return hipSuccess;
+    const uint32_t threads = n_regions * 16u;
+    hipLaunchKernelGGL(cluster_bits_kernel, dim3((threads + 255u) / 256u), dim3(256), 0, stream, vcs_mask, n_regions,
+                       cbits);
+    return hipGetLastError();
+}
+
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(pack_rgb8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, words, rgb, n);
@@ -1698,6 +1782,13 @@ hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hip
 }  // namespace vr
 
 #ifdef VR_DIAG
+extern "C" int vr_crawl_prof_fetch(unsigned int* out, unsigned int n) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vr_crawl_prof), sizeof(unsigned int) * 4 * (n < 16384u ? n : 16384u)) !=
+        hipSuccess)
+        return -1;
+    return 0;
+}
 extern "C" int vr_diag_fetch(unsigned long long* out, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vr_diag), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
