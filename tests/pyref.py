@@ -315,7 +315,8 @@ class Walk:
         if self.s.store == 1:
             # CuckooHashTable::lookupVoxel: key1 (+ val1), else key2 (+ val2)
             col = self.s.get(reg, key)
-            table = self.s.placement(self.s.region_index(reg), key) if col != EMPTY else 0
+            # (without a placement the bytes of a found key are counted as table 1's)
+            table = (self.s.placement(self.s.region_index(reg), key) if self.s.placement else 1) if col != EMPTY else 0
             self.bytes += 8 if table == 1 else (12 if table == 2 else 8)
             return col
         # performBinarySearch over the cluster's sorted keys (only after an existence

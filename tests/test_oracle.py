@@ -116,7 +116,8 @@ def _pyref_camera(cam):
 @pytest.mark.parametrize("store", [oracle.STORE_VCS, oracle.STORE_HASHTABLE])
 @pytest.mark.parametrize("algo", [oracle.ALGO_ORIGINAL, oracle.ALGO_LONGESTAXIS])
 def test_oracle_matches_python_restatement(store, algo):
-    """Two independent transcriptions of Renderer.cuh agree pixel for pixel."""
+    """Two independent transcriptions of Renderer.cuh agree pixel for pixel, and on each
+    ray's algorithmic bytes."""
     xyz, rgb = _golden_scene()
     W, H, scale = 256, 256, 12
     cam = oracle.reference_camera(W, H)
@@ -124,15 +125,12 @@ def test_oracle_matches_python_restatement(store, algo):
     px = rng.integers(0, W, 120)
     py = rng.integers(0, H, 120)
     sc = oracle.Scene(xyz, rgb, store)
-    ps = pyref.Scene(xyz, rgb, store)
+    ps = _pyref_scene(sc, xyz, rgb, store)
     for shadows, point in ((True, False), (False, True)):
         lit = oracle.lighting(use_shadows=shadows, use_point_light=point, light_position=(40.0, 90.0, 30.0))
         plit = pyref.Lighting(shadows, point, (40.0, 90.0, 30.0))
-        got, _ = sc.render_pixels(algo, cam, lit, W, H, scale, px, py)
-        for i in range(len(px)):
-            want = pyref.render_pixel(ps, plit, _pyref_camera(cam), W, H, int(px[i]), int(py[i]), scale,
-                                      algo == oracle.ALGO_LONGESTAXIS)
-            assert int(got[i]) == want, (int(px[i]), int(py[i]), hex(int(got[i])), hex(want))
+        _rays_agree(sc, ps, algo, cam, lit, plit, W, H, scale, px.astype(np.uint32), py.astype(np.uint32),
+                    where=(shadows, point))
 
 
 def test_oracle_matches_python_restatement_negative_and_translated():
@@ -143,15 +141,12 @@ def test_oracle_matches_python_restatement_negative_and_translated():
     tr = (-1.0, -0.5, 0.25)
     for store in (0, 1):
         sc = oracle.Scene(xyz, rgb, store)
-        ps = pyref.Scene(xyz, rgb, store)
-        px = rng.integers(0, 160, 60)
-        py = rng.integers(0, 120, 60)
+        ps = _pyref_scene(sc, xyz, rgb, store)
+        px = rng.integers(0, 160, 60).astype(np.uint32)
+        py = rng.integers(0, 120, 60).astype(np.uint32)
         for algo in (0, 1):
-            got, _ = sc.render_pixels(algo, cam, oracle.lighting(), 160, 120, 1, px, py, translation=tr)
-            for i in range(len(px)):
-                want = pyref.render_pixel(ps, pyref.Lighting(), _pyref_camera(cam), 160, 120, int(px[i]), int(py[i]),
-                                          1, algo == 0, translation=tr)
-                assert int(got[i]) == want
+            _rays_agree(sc, ps, algo, cam, oracle.lighting(), pyref.Lighting(), 160, 120, 1, px, py, translation=tr,
+                        where=store)
 
 
 def test_scene_geometry_rules():
