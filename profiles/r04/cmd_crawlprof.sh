@@ -1,6 +1,7 @@
+# crawl-pass profile (C5, both algorithms) from the VR_CRAWL_PROF build
 set -o pipefail
-mkdir -p gpurun_out/r04b
-VR_LIBRARY=voxelraymarcher_amd/ab/libvr_diag.so timeout -k 10 120 python profiles/crawl_prof.py C5 > gpurun_out/r04b/crawl_prof_C5.txt 2>&1 || exit 1
-VR_LIBRARY=voxelraymarcher_amd/ab/libvr_diag.so timeout -k 10 120 python profiles/crawl_prof.py C5 LONGEST_AXIS > gpurun_out/r04b/crawl_prof_C5_long.txt 2>&1 || exit 1
-cat gpurun_out/r04b/crawl_prof_C5*.txt
-bash profiles/r04/run_check.sh gpurun_out/r04b C2 C5 --no-tests
+O=${1:-gpurun_out/r04e}
+mkdir -p $O
+VR_LIBRARY=voxelraymarcher_amd/ab/libvr_cprof.so timeout -k 10 120 python profiles/crawl_prof.py C5 > $O/crawl_prof_C5.txt 2>&1 || { cat $O/crawl_prof_C5.txt; exit 1; }
+VR_LIBRARY=voxelraymarcher_amd/ab/libvr_cprof.so timeout -k 10 120 python profiles/crawl_prof.py C5 LONGEST_AXIS > $O/crawl_prof_C5_long.txt 2>&1 || exit 1
+cat $O/crawl_prof_C5*.txt

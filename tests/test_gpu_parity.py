@@ -339,3 +339,24 @@ def test_never_ending_walks():
         for algo in ALGOS:
             want = ref.render(int(algo), ocam, oracle_lighting_from(lit), 64, 64, 12)
             check_frame(xyz, rgb, store, algo, 64, 64, 12, cam=cam, lit=lit, want=want, defer_caps=(0, 16))
+
+
+@pytest.mark.parametrize("algo", ALGOS, ids=lambda a: a.name)
+def test_degenerate_light_direction(c1, algo):
+    """vr_lighting is plain data: a caller may hand a light direction that is not a unit
+    vector.  With (1e-6, 1e-6, 1e-6) (and colour 1e6, so that lit pixels are not 0) every
+    shadow step's EPSILON * d is ~1e-10: a cluster-skip crawl barely moves, and a crawl
+    that moved no coordinate would never finish.  GPU and oracle agree on every pixel and
+    byte, and the frame renders in well under the test's bound: no walk loop runs to the
+    crawl pass's 2^30-iteration hang guard ("Walks that never finish")."""
+    import time
+    lit = vr.setup_constant_values()
+    for i in range(3):
+        lit.light_dir[i] = 1e-6
+        lit.light_color[i] = 1e6
+    torch = pytest.importorskip("torch")
+    t0 = time.perf_counter()
+    for store in STORES:
+        check_frame(*c1, store, algo, 96, 96, vr.CONFIGS["C1"].scale, lit=lit, defer_caps=(0, 16))
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 60.0

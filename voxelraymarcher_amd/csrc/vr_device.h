@@ -186,7 +186,7 @@ struct Ctx {
     bool aborted = false;
     uint32_t bytes = 0;
     uint32_t ff = 0;     // (COUNT) crawl iterations credited in closed form (crawl_run)
-#ifdef VR_DIAG
+#ifdef VR_CRAWL_PROF
     uint32_t d_runs = 0, d_trips = 0;   // (diagnostic builds) crawl_run calls that applied steps, their loop trips
 #endif
 
@@ -198,7 +198,7 @@ struct Ctx {
     // n crawl iterations fast-forwarded: the existence read each of them stands for
     //  is credited, but the kernel never issues it
     __device__ __forceinline__ void count_ff(uint32_t n) {
-#ifdef VR_DIAG
+#ifdef VR_CRAWL_PROF
         ++d_runs;
         ff += COUNT ? 0u : n;
 #endif

@@ -22,11 +22,14 @@
 // VR_DIAG (profiling builds only, profiles/wave_counts.py): wave-level execution
 // counters -- one atomic per wave per counted event, from the wave's first
 // active lane.  Never part of the library build.
+#ifdef VR_CRAWL_PROF
+// per crawl record of the last crawl pass (profiles/crawl_prof.py): {shader cycles, plain
+// loop iterations (bit 31: walked from the start), crawl_run calls that applied steps, their
+// loop trips, start and end (s_memrealtime, 100 MHz), 0, 0}
+__device__ unsigned int g_vr_crawl_prof[16384 * 8];
+#endif
 #ifdef VR_DIAG
 __device__ unsigned long long g_vr_diag[32];
-// per crawl record of the last crawl pass: {shader cycles, plain loop iterations, crawl_run
-// calls that applied steps, their loop trips} (profiles/crawl_prof.py)
-__device__ unsigned int g_vr_crawl_prof[16384 * 4];
 #define VR_DIAG_COUNT(k)                                                              \
     do {                                                                             \
         if (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) \
@@ -112,20 +115,30 @@ __device__ __forceinline__ Crawl crawl_steps(f3 on, f3 d, int32_t vx, int32_t vy
     return r;
 }
 
-// A whole crawl through one cluster (crawl pass): from `o` -- the position a crawl
-// iteration stepped to from voxel q -- apply every further crawl iteration whose
-// result stays in q's cluster: runs of identical steps in one binade at once
-// (crawl_steps), and the steps between runs (across a binade edge, a tie from an
-// odd mantissa) one by one, exactly as the walk computes them, o_i + RN(EPSILON *
-// d_i).  Returns their number (0: not a crawl, or the next step leaves the
-// cluster); at most `room`.  The step that leaves the cluster is left to the walk
-// (performVoxelSpaceJump's hit normal reads its t values).  Pure arithmetic: a
-// crawl of 10^5..10^6 iterations costs a few dozen loop trips instead of as many
-// dependent mask loads.
+// A whole crawl (crawl pass): from `o` -- the position a crawl iteration stepped to from
+// voxel q -- apply every further crawl iteration: runs of identical steps in one binade
+// at once (crawl_steps), and the steps between runs (across a binade edge, a tie from an
+// odd mantissa) one by one, exactly as the walk computes them, o_i + RN(EPSILON * d_i).
+// Returns their number (0: not a crawl); at most `room`.  Pure arithmetic: a crawl of
+// 10^5..10^6 iterations costs a few dozen loop trips instead of as many dependent mask
+// loads.
+//   lbm == null (performVoxelSpaceJump's crawls): only the iterations whose results stay
+// in q's cluster; the step that leaves it is left to the walk (the jump's hit normal
+// reads its t values).
+//   lbm (the original DDA's crawls, whose skip steps feed no normal: Renderer.cuh:297-301,
+// SURVEY Q8): the region's cluster-existence bits.  A crawl does not end at its cluster's
+// face: an iteration that starts in an ABSENT cluster with the pinned axis still on its
+// plane (it never moves; the next cluster on the other axes shares that plane) is again a
+// skip with t = +-0 -- the same step.  So the crossing step is taken here as well, and
+// the crawl goes on through every absent cluster the ray meets in the region; it stops
+// after the step into a present cluster or out of the region (the walk resumes there).
+// Without this, each face crossing returned to the walk loop, which re-armed crawl
+// detection only after 8 single-step iterations: ~10-35 crossings per C5 record.
 __device__ __forceinline__ uint32_t crawl_run(f3& o, f3 d, int32_t qx, int32_t qy, int32_t qz, bool px, bool py,
-                                              bool pz, uint32_t room, uint32_t* trips = nullptr) {
+                                              bool pz, uint32_t room, const uint32_t* lbm = nullptr,
+                                              uint32_t* trips = nullptr) {
     const f3 c{kEps * d.x, kEps * d.y, kEps * d.z};
-    const int32_t lx = qx & ~7, ly = qy & ~7, lz = qz & ~7;
+    int32_t lx = qx & ~7, ly = qy & ~7, lz = qz & ~7;
     // an axis pinned on its cluster plane: direction negative, on the plane, unmoved by its step
     const bool pinned = (!px && (float)lx == o.x && o.x + c.x == o.x) ||
                         (!py && (float)ly == o.y && o.y + c.y == o.y) ||
@@ -135,10 +148,21 @@ __device__ __forceinline__ uint32_t crawl_run(f3& o, f3 d, int32_t qx, int32_t q
         return p.x >= (float)lx && p.x < (float)(lx + 8) && p.y >= (float)ly && p.y < (float)(ly + 8) &&
                p.z >= (float)lz && p.z < (float)(lz + 8);
     };
-    if (!inside(o)) return 0u;                  // the crawl iteration itself left the cluster
+    // p left the current cluster: go on crawling in p's cluster when it is in the region and absent
+    auto absent_next = [&](f3 p) -> bool {
+        if (!lbm || !(p.x >= 0.0f && p.x < 64.0f && p.y >= 0.0f && p.y < 64.0f && p.z >= 0.0f && p.z < 64.0f))
+            return false;
+        const int32_t ax = f2i(p.x), ay = f2i(p.y), az = f2i(p.z);
+        const uint32_t slot = (uint32_t)(((az >> 3) << 6) | ((ay >> 3) << 3) | (ax >> 3));
+        if ((lbm[slot >> 5] >> (slot & 31u)) & 1u) return false;
+        qx = ax; qy = ay; qz = az;
+        lx = ax & ~7; ly = ay & ~7; lz = az & ~7;
+        return true;
+    };
+    if (!inside(o) && !absent_next(o)) return 0u;   // the crawl iteration itself left the cluster
     uint32_t n = 0;
 #pragma unroll 1
-    for (uint32_t trip = 0; trip < 4096u && n < room; ++trip) {
+    for (uint32_t trip = 0; trip < 65536u && n < room; ++trip) {
         if (trips) ++*trips;
         const Crawl cw = crawl_steps(o, d, qx, qy, qz, px, py, pz, room - n);
         if (cw.m != 0u) {
@@ -148,7 +172,13 @@ __device__ __forceinline__ uint32_t crawl_run(f3& o, f3 d, int32_t qx, int32_t q
             if (n >= room) break;
         }
         const f3 o1{o.x + c.x, o.y + c.y, o.z + c.z};
-        if (!inside(o1)) break;
+        if (!inside(o1)) {
+            if (!lbm) break;
+            o = o1;                             // the crossing step (a skip in an absent cluster)
+            ++n;
+            if (!absent_next(o1)) break;
+            continue;
+        }
         o = o1;
         ++n;
     }
@@ -623,10 +653,10 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                 } else {
                     // Off the hot loop: fast-forward the identical crawl iterations
                     // exactly, then resume the walk (no region-entry step).
-#ifdef VR_DIAG
-                    const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters, &this->d_trips);
+#ifdef VR_CRAWL_PROF
+                    const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters, lbm, &this->d_trips);
 #else
-                    const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters);
+                    const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters, lbm);
 #endif
                     // none (not a real crawl, or its next step leaves the cluster): a few plain
                     // iterations, then re-arm
@@ -1032,8 +1062,8 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                             const f3 dd = to_f3(dL, dM, dS);
                             const i3 q = to_i3(qL, qM, qS);
                             const uint32_t n = crawl_run(on, dd, q.x, q.y, q.z, dd.x > 0.0f, dd.y > 0.0f, dd.z > 0.0f,
-                                                         kBudget - it
-#ifdef VR_DIAG
+                                                         kBudget - it, nullptr
+#ifdef VR_CRAWL_PROF
                                                          , &this->d_trips
 #endif
                                                          );
@@ -1445,7 +1475,7 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
         if (iters) *iters = w.iters;              // the walk's length (the work order's cost)
         bytes = w.bytes + 4u;                     // + the pixel write
         if (ff) *ff = w.ff;
-#ifdef VR_DIAG
+#ifdef VR_CRAWL_PROF
         if (dg) { dg[0] = w.iters - w.ff; dg[1] = w.d_runs; dg[2] = w.d_trips; }
 #endif
         if (w.aborted) {
@@ -1490,7 +1520,7 @@ __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v
     }
     bytes = w.bytes + 4u;
     ff = w.ff;
-#ifdef VR_DIAG
+#ifdef VR_CRAWL_PROF
     if (dg) { dg[0] = w.iters - r[9] - w.ff; dg[1] = w.d_runs; dg[2] = w.d_trips; }
 #endif
     if (w.aborted) {                              // never finishes (see shade)
@@ -1631,17 +1661,19 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
             }
         }
         uint32_t f = 0;
-#ifdef VR_DIAG
+#ifdef VR_CRAWL_PROF
         uint32_t dg[3] = {0, 0, 0};
-        const long long c0 = clock64();
+        const long long c0 = clock64(), t0 = wall_clock64();
         v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, dg, lbm)
                                          : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f, dg, lbm);
-        const long long c1 = clock64();
+        const long long c1 = clock64(), t1 = wall_clock64();
         if (i < 16384u) {
-            g_vr_crawl_prof[4 * i + 0] = (uint32_t)min(c1 - c0, 0xFFFFFFFFll);
-            g_vr_crawl_prof[4 * i + 1] = dg[0] | (amb ? 0x80000000u : 0u);
-            g_vr_crawl_prof[4 * i + 2] = dg[1];
-            g_vr_crawl_prof[4 * i + 3] = dg[2];
+            g_vr_crawl_prof[8 * i + 0] = (uint32_t)min(c1 - c0, 0xFFFFFFFFll);
+            g_vr_crawl_prof[8 * i + 1] = dg[0] | (amb ? 0x80000000u : 0u);
+            g_vr_crawl_prof[8 * i + 2] = dg[1];
+            g_vr_crawl_prof[8 * i + 3] = dg[2];
+            g_vr_crawl_prof[8 * i + 4] = (uint32_t)t0;
+            g_vr_crawl_prof[8 * i + 5] = (uint32_t)t1;
         }
 #else
         v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, nullptr, lbm)
@@ -1781,14 +1813,16 @@ hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hip
 
 }  // namespace vr
 
-#ifdef VR_DIAG
+#ifdef VR_CRAWL_PROF
 extern "C" int vr_crawl_prof_fetch(unsigned int* out, unsigned int n) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vr_crawl_prof), sizeof(unsigned int) * 4 * (n < 16384u ? n : 16384u)) !=
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vr_crawl_prof), sizeof(unsigned int) * 8 * (n < 16384u ? n : 16384u)) !=
         hipSuccess)
         return -1;
     return 0;
 }
+#endif
+#ifdef VR_DIAG
 extern "C" int vr_diag_fetch(unsigned long long* out, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vr_diag), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
