@@ -185,6 +185,8 @@ struct Ctx {
     uint32_t iters = 0;
     bool aborted = false;
     uint32_t bytes = 0;
+    // crawl pass (BUDGET == kCrawlBudget) with the scene cached in LDS: the region table
+    const uint32_t* lrt = nullptr;
     uint32_t ff = 0;     // (COUNT) crawl iterations credited in closed form (crawl_run)
 #ifdef VR_CRAWL_PROF
     uint32_t d_runs = 0, d_trips = 0;   // (diagnostic builds) crawl_run calls that applied steps, their loop trips
@@ -222,6 +224,9 @@ struct Ctx {
         uint32_t mc = (uint32_t)s.min_coord;
         uint32_t ux = (uint32_t)r.x - mc, uy = (uint32_t)r.y - mc, uz = (uint32_t)r.z - mc;
         count(4);
+        if constexpr (BUDGET == kCrawlBudget) {
+            if (lrt) return lrt[ux + uy * s.D + uz * s.D * s.D];
+        }
         return s.region_slot[ux + uy * s.D + uz * s.D * s.D];
     }
 
@@ -230,6 +235,9 @@ struct Ctx {
     __device__ __forceinline__ uint32_t region_at_nocount(i3 r) const {
         uint32_t mc = (uint32_t)s.min_coord;
         uint32_t ux = (uint32_t)r.x - mc, uy = (uint32_t)r.y - mc, uz = (uint32_t)r.z - mc;
+        if constexpr (BUDGET == kCrawlBudget) {
+            if (lrt) return lrt[ux + uy * s.D + uz * s.D * s.D];
+        }
         return s.region_slot[ux + uy * s.D + uz * s.D * s.D];
     }
 

@@ -453,6 +453,7 @@ vr::KScene kscene(const vr_scene* s) {
     k.ht_slots = (const uint2*)s->ht_slots.p;
     k.D = s->D;
     k.min_coord = s->min_coord;
+    k.n_regions = s->n_regions;
     return k;
 }
 
@@ -532,13 +533,6 @@ struct SlotRing {
             bool valid = false;
         };
         std::vector<Order> ord;
-        // the XCD-aware grid order of one grid size (made on the host once, then reused)
-        struct XcdOrder {
-            uint32_t gx = 0, gy = 0, w = 0;
-            uint32_t* order = nullptr;
-        };
-        XcdOrder xo[4];
-        uint32_t xo_next = 0;
         bool any = false;                  // the device's previous launch: its stream and slot
         hipStream_t last_stream = nullptr;
         uint32_t last_idx = 0;
@@ -635,62 +629,6 @@ uint32_t order_refresh() {
     }();
     return r;
 }
-// XCD-aware grid order (VR_XCD_CHUNK tile-group columns per chunk; 0 = plain grid order).
-// Workgroups b and b + 8 share an XCD (round-robin dealing, observed; speed only, never
-// correctness: MI355X_MICROARCH.md "Workgroup dispatch"), and each XCD has its own 4 MB L2.
-// In plain grid order every XCD renders thin slices of every part of the view, so every L2
-// holds the whole view's working set.  This permutation gives XCD label x = b % 8 the tile
-// groups of the column chunks c with c % 8 == x, row by row (top to bottom, as grid order
-// dispatches them): each L2 sees chunks of 1/8 of the view, spread over the frame so the
-// labels' loads stay balanced.  Labels whose chunks hold more tile groups than the label
-// gets blocks hand the rest to the others at the end.
-uint32_t xcd_chunk() {
-    static const uint32_t w = [] {
-        const char* e = std::getenv("VR_XCD_CHUNK");
-        const long v = e ? std::strtol(e, nullptr, 10) : 0;
-        return (uint32_t)(v >= 0 && v <= 4096 ? v : 0);
-    }();
-    return w;
-}
-std::vector<uint32_t> make_xcd_order(uint32_t gx, uint32_t gy, uint32_t w) {
-    const uint32_t n = gx * gy, nch = (gx + w - 1) / w;
-    std::vector<uint32_t> seq[8];
-    for (uint32_t r = 0; r < gy; ++r)
-        for (uint32_t c = 0; c < nch; ++c)
-            for (uint32_t k = 0; k < w && c * w + k < gx; ++k) seq[c % 8].push_back(r << 16 | (c * w + k));
-    std::vector<uint32_t> order(n), pool;
-    size_t used[8] = {0};
-    uint32_t cnt[8] = {0};
-    for (uint32_t b = 0; b < n; ++b) ++cnt[b % 8];
-    for (uint32_t x = 0; x < 8; ++x)
-        for (size_t i = cnt[x]; i < seq[x].size(); ++i) pool.push_back(seq[x][i]);
-    size_t pi = 0;
-    for (uint32_t b = 0; b < n; ++b) {
-        const uint32_t x = b % 8;
-        order[b] = used[x] < std::min<size_t>(cnt[x], seq[x].size()) ? seq[x][used[x]++] : pool[pi++];
-    }
-    return order;
-}
-// The device buffer of the XCD-aware order for a grid (the device's lock is held).
-uint32_t* xcd_order(SlotRing::Dev& D, uint32_t gx, uint32_t gy, uint32_t w) {
-    for (auto& o : D.xo)
-        if (o.order && o.gx == gx && o.gy == gy && o.w == w) return o.order;
-    auto& o = D.xo[D.xo_next++ % 4];
-    if (o.order) {
-        if (hipDeviceSynchronize() != hipSuccess) return nullptr;     // (a launch may still read it)
-        (void)hipFree(o.order);
-        o = SlotRing::Dev::XcdOrder{};
-    }
-    const std::vector<uint32_t> h = make_xcd_order(gx, gy, w);
-    void* p = nullptr;
-    if (hipMalloc(&p, h.size() * sizeof(uint32_t)) != hipSuccess) return nullptr;
-    if (hipMemcpy(p, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(p);
-        return nullptr;
-    }
-    o.gx = gx; o.gy = gy; o.w = w; o.order = (uint32_t*)p;
-    return o.order;
-}
 // VR_CRAWL_RPW (A/B runs): crawl records per wave for every launch instead of 4 / 8.
 uint32_t crawl_rpw_override() {
     static const uint32_t r = [] {
@@ -699,6 +637,18 @@ uint32_t crawl_rpw_override() {
         return (uint32_t)(v >= 1 && v <= 64 ? v : 0);
     }();
     return r;
+}
+// VR_CRAWL_SCENE_LDS=1 (A/B runs): the crawl pass caches the scene's region table and
+// cluster bits in each workgroup's LDS when they fit.  Off by default: measured no faster
+// than the per-record bit slots for a lone C5 frame (0.806 vs 0.801 ms) and slower with
+// frames in flight (0.677 vs 0.636 ms per frame; one 108-KB workgroup per CU),
+// profiles/r04/crawl/scene_lds_ab.txt.
+bool crawl_scene_lds_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("VR_CRAWL_SCENE_LDS");
+        return e && e[0] == '1';
+    }();
+    return on;
 }
 bool order_enabled() {
     static const bool on = [] {
@@ -776,11 +726,14 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         remake = !match || ++O.age >= order_refresh();
         v.cost = remake ? O.cost : nullptr;
     }
-    // grid order: the XCD-aware permutation when enabled (not while the stream is captured:
-    // its first use of a grid size allocates and copies synchronously)
-    if (!v.order && xcd_chunk() && n > 1 && cap == hipStreamCaptureStatusNone)
-        v.order = xcd_order(D, gx, gy, std::min(xcd_chunk(), gx));
-    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, kscene(s), v, st, vr::crawl_grid(expect, v.crawl_rpw));
+    // crawl pass: the scene cached in each workgroup's LDS when it fits and records are
+    // expected (a hint from an earlier launch: any shape renders the same pixels)
+    const vr::KScene ks = kscene(s);
+    v.crawl_scene_lds = (s->store == VR_STORE_VCS && expect > 0 && crawl_scene_lds_enabled() && vr::crawl_lds_fits(ks))
+                            ? 1u : 0u;
+    const uint32_t cwgs = v.crawl_scene_lds ? vr::crawl_grid_scene_lds(expect, v.crawl_rpw)
+                                            : vr::crawl_grid(expect, v.crawl_rpw);
+    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs);
     if (e == hipSuccess && remake) {
         // (on a side stream instead -- one more stream than the box's 4 hardware queues
         // serialised the two render streams: C2 0.1124 -> 0.1277 ms per frame in flight,

@@ -64,6 +64,7 @@ struct KScene {
     const uint2* ht_slots;
     uint32_t D;
     int32_t min_coord;
+    uint32_t n_regions;
 };
 
 // Per-launch view: camera, lighting, scene transform and the row mapping.
@@ -100,6 +101,9 @@ struct KView {
     uint32_t defer_cap;
     uint32_t crawl_rewalk;    // 1: deferred crawls are walked from the pixel's start (VR_KERNEL_TILE_REWALK)
     uint32_t crawl_rpw;       // crawl records per wave (0 = 4): 4 for a lone frame, 8 with frames in flight
+    // crawl pass: 1 = each workgroup caches the scene's region table and cluster-existence
+    // bits in LDS (crawl_lds_bytes, vr_march.hip crawl_kernel); 0 = per-record bit slots
+    uint32_t crawl_scene_lds;
     uint32_t* defer_stat;     // host-mapped word: the crawl pass writes its record count there (grid sizing)
     // Tile-pass work order ("Heaviest tiles first"): workgroup i of the grid
     // renders tile order[i] = (tile row << 16 | tile column) -- a permutation of the grid
@@ -134,6 +138,13 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
                         hipStream_t stream, uint32_t crawl_wgs);
 // Crawl-pass grid for a launch that expects about `records` deferred pixels.
 uint32_t crawl_grid(uint32_t records, uint32_t rpw);
+// The crawl pass's shape (vr_march.hip): threads per workgroup and dynamic LDS bytes for the
+// scene-cached mode (v.crawl_scene_lds) or the per-record mode; crawl_lds_fits: the scene's
+// region table and cluster bits fit one workgroup's LDS.
+uint32_t crawl_threads(bool scene_lds);
+uint32_t crawl_lds_bytes(const KScene& s, bool scene_lds);
+bool crawl_lds_fits(const KScene& s);
+uint32_t crawl_grid_scene_lds(uint32_t records, uint32_t rpw);
 // vcs_cbits of a VCS scene from its mask records (one thread per 32 cluster slots).
 hipError_t launch_cluster_bits(const uint2* vcs_mask, uint32_t n_regions, uint32_t* cbits, hipStream_t stream);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);

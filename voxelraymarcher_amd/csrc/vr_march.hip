@@ -100,9 +100,13 @@ __device__ __forceinline__ Crawl crawl_steps(f3 on, f3 d, int32_t vx, int32_t vy
     bool pinned = false;
     float m = (float)room;
     f3 dl{0.0f, 0.0f, 0.0f};
-    // one axis at a time (a rolled loop keeps its temporaries from stacking up
-    // on the walk's live registers: this cold block sets the kernel's VGPR count)
+    // (crawl kernel only: its register budget is not the tile pass's, so the axes are
+    // unrolled -- VR_CRAWL_ROLLED keeps the rolled loop for A/B)
+#ifdef VR_CRAWL_ROLLED
 #pragma unroll 1
+#else
+#pragma unroll
+#endif
     for (uint32_t a = 0; a < 3u; ++a) {
         float delta;
         if (!crawl_axis(comp(on, a), comp(d, a), a == 0 ? vx : (a == 1 ? vy : vz), a == 0 ? px : (a == 1 ? py : pz),
@@ -309,6 +313,8 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
     // clusters: a skip step reads one LDS word instead.
     uint32_t* lbm = nullptr;
     uint32_t bm_reg = kNone;
+    // (crawl pass, scene cached in LDS) every region's cluster-existence bits, 16 words each
+    const uint32_t* lbits = nullptr;
 
     // rayMarchVoxelGrid (Renderer.cuh:260-336) and, SHADOW, shadowRayMarchVoxelGrid (:100-172).
     // The cluster-skip step (:290-306) and the voxel step (:318-331) share one
@@ -384,12 +390,22 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             // the region's mask words as a 32-bit byte offset from the scene's (uniform)
             // mask array: the loads take the SGPR-base form (one VGPR, no 64-bit add)
             const uint32_t moff = reg << 16;
-            if (CRAWL && lbm && reg != bm_reg) {      // the region's cluster-existence bits into LDS
-                const uint4* src = reinterpret_cast<const uint4*>(s.vcs_cbits + (size_t)reg * 16u);
-                const uint4 b0 = src[0], b1 = src[1], b2 = src[2], b3 = src[3];
-                uint4* dst = reinterpret_cast<uint4*>(lbm);
-                dst[0] = b0; dst[1] = b1; dst[2] = b2; dst[3] = b3;
-                bm_reg = reg;
+            // (crawl pass) the region's cluster-existence bits in LDS: the workgroup's copy of
+            // the scene's, or this lane's slot, refilled when the walk enters another region
+            const uint32_t* bits = nullptr;
+            if constexpr (CRAWL) {
+                if (lbits) {
+                    bits = lbits + reg * 16u;
+                } else if (lbm) {
+                    if (reg != bm_reg) {
+                        const uint4* src = reinterpret_cast<const uint4*>(s.vcs_cbits + (size_t)reg * 16u);
+                        const uint4 b0 = src[0], b1 = src[1], b2 = src[2], b3 = src[3];
+                        uint4* dst = reinterpret_cast<uint4*>(lbm);
+                        dst[0] = b0; dst[1] = b1; dst[2] = b2; dst[3] = b3;
+                        bm_reg = reg;
+                    }
+                    bits = lbm;
+                }
             }
             // Straight-line body with one exit: the hit test, the region test of
             // the stepped position and the iteration budget are folded into a
@@ -466,7 +482,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                             const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
                             if constexpr (CRAWL) {
                                 // (crawl pass) cluster slot wi >> 4 absent per the LDS bits: no load
-                                const bool pres = !lbm || ((lbm[wi >> 9] >> ((wi >> 4) & 31u)) & 1u);
+                                const bool pres = !bits || ((bits[wi >> 9] >> ((wi >> 4) & 31u)) & 1u);
                                 blk = Blk{0u, kNone};
                                 if (pres)
                                     blk = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) +
@@ -654,9 +670,9 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                     // Off the hot loop: fast-forward the identical crawl iterations
                     // exactly, then resume the walk (no region-entry step).
 #ifdef VR_CRAWL_PROF
-                    const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters, lbm, &this->d_trips);
+                    const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters, bits, &this->d_trips);
 #else
-                    const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters, lbm);
+                    const uint32_t n = crawl_run(o, d, qx, qy, qz, px, py, pz, kBudget - this->iters, bits);
 #endif
                     // none (not a real crawl, or its next step leaves the cluster): a few plain
                     // iterations, then re-arm
@@ -938,6 +954,38 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                                                      bool& tail, uint32_t& hcol, uint32_t& hcode) {
         const float dL = ax3<PL>(ds), dM = ax3<PM>(ds), dS = ax3<PS>(ds);
         auto dv = [](float n, float d) { return UNIT ? n * d : n / d; };
+        // VR_LONG_FAST_DIV: n / d by div_fast with the reciprocal made right here from a
+        // pinned copy of d (an empty asm on it: never hoisted into a loop-carried VGPR, the
+        // spill growth that sank every hoisted-reciprocal variant), IEEE division for lanes
+        // outside div_fast's domain (one ballot).  Numerators here are never -0 (x - x = +0).
+#ifndef VR_LONG_FAST_DIV
+#define VR_LONG_FAST_DIV 0
+#endif
+        auto dv3 = [&](float n0, float d0, float n1, float d1, float n2, float d2, float& q0, float& q1, float& q2) {
+            if (UNIT || !VR_LONG_FAST_DIV) {
+                q0 = dv(n0, d0); q1 = dv(n1, d1); q2 = dv(n2, d2);
+                return;
+            }
+            float e0 = d0, e1 = d1, e2 = d2;
+            asm volatile("" : "+v"(e0), "+v"(e1), "+v"(e2));
+            const Rcp r0 = rcp_setup(e0), r1 = rcp_setup(e1), r2 = rcp_setup(e2);
+            q0 = div_fast(n0, r0); q1 = div_fast(n1, r1); q2 = div_fast(n2, r2);
+            auto ok = [](float n, const Rcp& r) { return __float_as_uint(n) == 0u || div_fast_ok(n, r); };
+            const bool good = ok(n0, r0) && ok(n1, r1) && ok(n2, r2);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(!good) != 0, 0)) {
+                q0 = good ? q0 : n0 / d0; q1 = good ? q1 : n1 / d1; q2 = good ? q2 : n2 / d2;
+            }
+        };
+        auto dv1 = [&](float n, float d) {
+            if (UNIT || !VR_LONG_FAST_DIV) return dv(n, d);
+            float e = d;
+            asm volatile("" : "+v"(e));
+            const Rcp r = rcp_setup(e);
+            float q = div_fast(n, r);
+            const bool good = __float_as_uint(n) == 0u || div_fast_ok(n, r);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64(!good) != 0, 0)) q = good ? q : n / d;
+            return q;
+        };
         const bool posL = (cls >> (2 * PL)) & 1u, posM = (cls >> (2 * PM)) & 1u, posS = (cls >> (2 * PS)) & 1u;
         const bool negL = (cls >> (2 * PL + 1)) & 1u, negM = (cls >> (2 * PM + 1)) & 1u;
         const int32_t offL = posL ? 8 : 0, offM = posM ? 8 : 0, offS = posS ? 8 : 0;
@@ -1010,7 +1058,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                 const bool hasM = aM != 0, hasS = aS != 0;
                 bool sfirst = false;
                 if (hasM && hasS) {
-                    const float t1 = dv((mid_floor ? floorf(oM) : ceilf(oM)) - oM, dM);
+                    const float t1 = dv1((mid_floor ? floorf(oM) : ceilf(oM)) - oM, dM);
                     const float sp = oS + dS * t1;
                     sfirst = f2i(floorf(sp)) - gS != 0;
                 }
@@ -1031,7 +1079,9 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                     bL = (gL / 8) * 8; bM = (gM / 8) * 8; bS = (gS / 8) * 8;
                 }
                 const int32_t nL = bL + offL, nM = bM + offM, nS = bS + offS;
-                const auto t = xyz(dv((float)nL - oL, dL), dv((float)nM - oM, dM), dv((float)nS - oS, dS));
+                float jL, jM, jS;
+                dv3((float)nL - oL, dL, (float)nM - oM, dM, (float)nS - oS, dS, jL, jM, jS);
+                const auto t = xyz(jL, jM, jS);
                 const float tm0 = fminf(t.c[0], fminf(t.c[1], t.c[2]));
                 const float tMin = tm0 + kEps;
                 nj = t.c[0] == tMin ? 0u : (t.c[1] == tMin ? 1u : 2u);
@@ -1141,7 +1191,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             }
             if (jumping && stop == 3u) {
                 // landed in an existing cluster without a hit: CONTINUE_VAL (:740-750)
-                const float tNext = dv((posL ? ceilf(oL) : floorf(oL)) - oL, dL);
+                const float tNext = dv1((posL ? ceilf(oL) : floorf(oL)) - oL, dL);
                 rL = oL + (tNext + kEps) * dL; rM = oM + (tNext + kEps) * dM; rS = oS + (tNext + kEps) * dS;
             }
             if (!jumping) {
@@ -1452,6 +1502,21 @@ __device__ __forceinline__ uint32_t defer_rewalk(const KView& v, uint32_t x, uin
     return kDeferMarker;
 }
 
+// The crawl pass's LDS for one record lane: its bit slot (per-record mode) or the
+// workgroup's copy of the scene's region table and cluster bits (scene-cached mode).
+struct CrawlLds {
+    uint32_t* lbm = nullptr;
+    const uint32_t* lrt = nullptr;
+    const uint32_t* lbits = nullptr;
+};
+template <class W>
+__device__ __forceinline__ void attach(W& w, const CrawlLds* cl) {
+    if (!cl) return;
+    w.lbm = cl->lbm;
+    w.lrt = cl->lrt;
+    w.lbits = cl->lbits;
+}
+
 // The body of rayMarchSceneOriginal / rayMarchSceneJumpAxis (Renderer.cuh:1033-1063)
 // for pixel (x, local row l): colour, algorithmic bytes (+4 for the pixel write).
 // Tile pass (!CRAWL): a pixel deferred to the crawl pass -- a crawl record, or a
@@ -1462,14 +1527,14 @@ __device__ __forceinline__ uint32_t defer_rewalk(const KView& v, uint32_t x, uin
 template <int STORE, int ALGO, bool COUNT, bool CRAWL>
 __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint32_t x, uint32_t l,
                                           uint32_t& bytes, uint32_t* iters = nullptr, uint32_t* ff = nullptr,
-                                          uint32_t* dg = nullptr, uint32_t* lbm = nullptr) {
+                                          uint32_t* dg = nullptr, const CrawlLds* cl = nullptr) {
     uint32_t col = 0;
     bytes = 0;
     if (ff) *ff = 0;
     f3 ro, rd;
     if (pixel_ray<true>(v, x, l, ro, rd)) {
         Walker<STORE, COUNT, CRAWL> w(s, v);
-        w.lbm = lbm;
+        attach(w, cl);
         Hit h;
         if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
         if (iters) *iters = w.iters;              // the walk's length (the work order's cost)
@@ -1497,10 +1562,10 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
 template <int STORE, int ALGO, bool COUNT>
 __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v,
                                                  const uint32_t* r, uint32_t& bytes, uint32_t& ff,
-                                                 uint32_t* dg = nullptr, uint32_t* lbm = nullptr) {
+                                                 uint32_t* dg = nullptr, const CrawlLds* cl = nullptr) {
     const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
     Walker<STORE, COUNT, true> w(s, v);
-    w.lbm = lbm;
+    attach(w, cl);
     w.iters = r[9];
     w.bytes = r[10];
     const f3 o{__uint_as_float(r[2]), __uint_as_float(r[3]), __uint_as_float(r[4])};
@@ -1609,21 +1674,44 @@ __global__ __launch_bounds__(1024) void order_kernel(const uint32_t* __restrict_
 #endif
 constexpr uint32_t kCrawlRpw = VR_CRAWL_RPW;
 constexpr uint32_t kCrawlMaxRpw = 16;     // records per wave with an LDS bitmap slot
+// Workgroup shapes: per-record mode 2 waves (as the tile pass); scene-cached mode 8 waves,
+// one workgroup per CU (its LDS copy of the scene is up to kCrawlSceneLdsMax bytes).
+constexpr uint32_t kCrawlWaves = 2, kCrawlSceneWaves = 8;
+constexpr uint32_t kCrawlSceneLdsMax = 144u * 1024u;
+// Dynamic LDS layout (16-B aligned carve-outs, cdna_hip_programming.md Guideline 17):
+//   [0, 16)        record count, overflow count
+//   per-record:    16 words per record lane (kCrawlMaxRpw per wave)
+//   scene-cached:  the region table (D^3 words, padded to 16 B), then every region's 16
+//                  cluster-bit words
+__device__ __forceinline__ uint32_t rt_words_padded(const KScene& s) {
+    return ((s.D * s.D * s.D) + 3u) & ~3u;
+}
 template <int STORE, int ALGO, bool COUNT>
-__global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
-    __shared__ uint32_t n_lds, ovf_lds;
-    // per record lane: the cluster-existence bits of the region its walk is in (VCS)
-    __shared__ __attribute__((aligned(16))) uint32_t lbm_all[(256 / 64) * kCrawlMaxRpw * 16];
+__global__ __launch_bounds__(64 * kCrawlSceneWaves) void crawl_kernel(KScene s, KView v) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
     if (threadIdx.x == 0) {
-        n_lds = v.defer[0];
-        ovf_lds = v.defer[2];
+        dyn[0] = v.defer[0];
+        dyn[1] = v.defer[2];
     }
     __syncthreads();
-    const uint32_t total = n_lds, overflow = ovf_lds;
+    const uint32_t total = dyn[0], overflow = dyn[1];
     // what this launch deferred, for the host's grid size of later launches (a hint only)
     if (blockIdx.x == 0 && threadIdx.x == 0 && v.defer_stat) *v.defer_stat = total + overflow;
     if (total == 0u && overflow == 0u) return;   // nothing deferred (the usual case): no reset needed
     const uint32_t n = min(total, v.defer_cap);
+    CrawlLds cl;
+    if (STORE == STORE_VCS && v.crawl_scene_lds) {
+        // the scene's region table and cluster bits, once per workgroup: a record's walk then
+        // reads global memory only for present clusters' mask words and the hit's colour
+        const uint32_t nrt = s.D * s.D * s.D, off = 4u + rt_words_padded(s), nb = s.n_regions * 16u;
+        for (uint32_t i = threadIdx.x; i < nrt; i += blockDim.x) dyn[4 + i] = s.region_slot[i];
+        const uint4* src = reinterpret_cast<const uint4*>(s.vcs_cbits);
+        uint4* dst = reinterpret_cast<uint4*>(dyn + off);
+        for (uint32_t i = threadIdx.x; i < nb / 4u; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+        cl.lrt = dyn + 4;
+        cl.lbits = dyn + off;
+    }
     unsigned long long bytes = 0, ffs = 0;
     // kCrawlRpw records per wave at a time (lanes 0 .. kCrawlRpw-1): each record is a long
     // chain of dependent iterations, and the lanes of a wave take different paths through
@@ -1634,9 +1722,9 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
     const uint32_t rpw = v.crawl_rpw ? v.crawl_rpw : kCrawlRpw;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, wlane = threadIdx.x & 63u;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    uint32_t* lbm = (STORE == STORE_VCS && s.vcs_cbits && rpw <= kCrawlMaxRpw && wlane < rpw)
-                        ? lbm_all + ((threadIdx.x >> 6) * kCrawlMaxRpw + wlane) * 16u
-                        : nullptr;
+    if (STORE == STORE_VCS && !v.crawl_scene_lds && s.vcs_cbits && rpw <= kCrawlMaxRpw && wlane < rpw &&
+        blockDim.x <= 64u * kCrawlWaves)
+        cl.lbm = dyn + 4 + ((threadIdx.x >> 6) * kCrawlMaxRpw + wlane) * 16u;
     for (uint32_t i = wave * rpw + wlane; wlane < rpw && i < n; i += nwaves * rpw) {
         uint32_t* r = v.defer + 4 + (size_t)i * kDeferRecWords;
         uint32_t b;
@@ -1664,8 +1752,8 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
 #ifdef VR_CRAWL_PROF
         uint32_t dg[3] = {0, 0, 0};
         const long long c0 = clock64(), t0 = wall_clock64();
-        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, dg, lbm)
-                                         : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f, dg, lbm);
+        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, dg, &cl)
+                                         : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f, dg, &cl);
         const long long c1 = clock64(), t1 = wall_clock64();
         if (i < 16384u) {
             g_vr_crawl_prof[8 * i + 0] = (uint32_t)min(c1 - c0, 0xFFFFFFFFll);
@@ -1676,8 +1764,8 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
             g_vr_crawl_prof[8 * i + 5] = (uint32_t)t1;
         }
 #else
-        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, nullptr, lbm)
-                                         : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f, nullptr, lbm);
+        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, nullptr, &cl)
+                                         : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f, nullptr, &cl);
 #endif
         bytes += b;
         ffs += f;
@@ -1688,7 +1776,13 @@ __global__ __launch_bounds__(256) void crawl_kernel(KScene s, KView v) {
         for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (size_t)gridDim.x * blockDim.x) {
             if (v.out[i] != kDeferMarker) continue;
             uint32_t b, f = 0;
-            v.out[i] = shade<STORE, ALGO, COUNT, true>(s, v, (uint32_t)(i % v.W), (uint32_t)(i / v.W), b, nullptr, &f);
+            // (the scene-cached LDS is the workgroup's: usable by every lane; a per-record bit
+            // slot is not this lane's)
+            CrawlLds clo;
+            clo.lrt = cl.lrt;
+            clo.lbits = cl.lbits;
+            v.out[i] = shade<STORE, ALGO, COUNT, true>(s, v, (uint32_t)(i % v.W), (uint32_t)(i / v.W), b, nullptr, &f,
+                                                       nullptr, &clo);
             bytes += b;
             ffs += f;
         }
@@ -1738,8 +1832,25 @@ __global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __rest
 // flight, profiles/r03/ab_crawl_rpw.txt), at least 64 workgroups.  The host sizes it from
 // the count an earlier launch of the device wrote to defer_stat: a launch that defers
 // nothing (C2-C4) keeps the small grid (1024 empty workgroups cost C2 0.6 %).
+uint32_t crawl_threads(bool scene_lds) { return 64u * (scene_lds ? kCrawlSceneWaves : kCrawlWaves); }
+uint32_t crawl_lds_bytes(const KScene& s, bool scene_lds) {
+    if (!scene_lds) return 16u + kCrawlWaves * kCrawlMaxRpw * 16u * 4u;
+    const uint64_t nrt = (uint64_t)s.D * s.D * s.D;
+    return (uint32_t)std::min<uint64_t>(16u + 4u * (((nrt + 3u) & ~3ull) + (uint64_t)s.n_regions * 16u), 0xFFFFFFFFu);
+}
+bool crawl_lds_fits(const KScene& s) {
+    const uint64_t nrt = (uint64_t)s.D * s.D * s.D;
+    return s.vcs_cbits && 16u + 4u * (((nrt + 3u) & ~3ull) + (uint64_t)s.n_regions * 16u) <= kCrawlSceneLdsMax;
+}
+// scene-cached mode: one 8-wave workgroup per CU holds rpw records per wave; waves loop over
+// further records when there are more than 256 workgroups' worth
+uint32_t crawl_grid_scene_lds(uint32_t records, uint32_t rpw) {
+    rpw = rpw ? rpw : kCrawlRpw;
+    const uint64_t per = (uint64_t)kCrawlSceneWaves * rpw;
+    return (uint32_t)std::min<uint64_t>(std::max<uint64_t>((records + per - 1) / per, 1u), 256u);
+}
 uint32_t crawl_grid(uint32_t records, uint32_t rpw) {
-    const uint32_t waves_per_wg = kTilesX * kTilesY;
+    const uint32_t waves_per_wg = kCrawlWaves;
     rpw = rpw ? rpw : kCrawlRpw;
     const uint64_t waves = ((uint64_t)records * 5u / 4u + rpw - 1u) / rpw;
     const uint64_t wgs = (waves + waves_per_wg - 1u) / waves_per_wg;
@@ -1774,10 +1885,19 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
     dim3 block(64u * kTilesX * kTilesY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     const dim3 cgrid(crawl_wgs ? crawl_wgs : 64u);
+    const bool scene_lds = v.crawl_scene_lds != 0;
+    const dim3 cblock(crawl_threads(scene_lds));
+    const uint32_t clds = crawl_lds_bytes(s, scene_lds);
 #define VR_LAUNCH(ST, AL, CT)                                                                     \
     do {                                                                                           \
         hipLaunchKernelGGL((march_kernel<ST, AL, CT>), grid, block, 0, stream, s, v);              \
-        if (v.defer && !kNoCrawlPass) hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, block, 0, stream, s, v); \
+        if (v.defer && !kNoCrawlPass) {                                                            \
+            static const hipError_t attr = hipFuncSetAttribute(                                    \
+                reinterpret_cast<const void*>(&crawl_kernel<ST, AL, CT>),                          \
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCrawlSceneLdsMax);                \
+            if (attr != hipSuccess) return attr;                                                   \
+            hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, cblock, clds, stream, s, v);     \
+        }                                                                                          \
     } while (0)
 #ifdef VR_ISA_ONLY
     // ISA-inspection builds (csrc/Makefile isa1, profiles/loop_isa.py): one kernel pair
