@@ -7,6 +7,11 @@ by the slowest rank (its gather to rank 0 runs beside the next frame, DESIGN.md 
 so max over ranks of the per-rank frame time is the projection -- without the RCCL
 gather, which no one-GPU box can run (profiles/r03/rccl/).
 
+The single-frame latency projection (round 4): each rank's ONE frame alone on the GPU
+(render of its bands + RGB8 pack, then synchronise), median over --latency-reps launches in
+grid order (a first render) and with the learned heaviest-first order; the N-GPU latency is
+the slowest rank's (the gather to rank 0 adds its own ~27 us per rank over xGMI).
+
   python profiles/rank_projection.py [--config C5] [--world 8] [--steps 100]"""
 import argparse
 import json
@@ -14,23 +19,31 @@ import os
 import sys
 import time
 
-import torch
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-
-import voxelraymarcher_amd as vr  # noqa: E402
-from voxelraymarcher_amd.tiles import BandGather, owned_rows  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--config", default="C5")
 p.add_argument("--world", type=int, default=8)
 p.add_argument("--steps", type=int, default=100)
 p.add_argument("--warmup", type=int, default=20)
-p.add_argument("--frames-in-flight", type=int, default=0)
+p.add_argument("--frames-in-flight", type=int, default=0, help="default: tiles.pipeline_depth (bench.py's)")
 p.add_argument("--ranks", default="", help="comma-separated subset of ranks (default: all)")
 p.add_argument("--band-rows", type=int, default=8)
+p.add_argument("--latency-reps", type=int, default=30)
 a = p.parse_args()
+
+from voxelraymarcher_amd.tiles import pipeline_depth, pipeline_hw_queues  # noqa: E402  (no GPU yet)
+depth = a.frames_in_flight or pipeline_depth(a.config)
+_q = pipeline_hw_queues(depth)
+if _q and not (os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() and int(os.environ["GPU_MAX_HW_QUEUES"]) >= _q):
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_q)      # as bench.py: before the HIP runtime starts
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import voxelraymarcher_amd as vr  # noqa: E402
+from voxelraymarcher_amd.tiles import BandGather, owned_rows  # noqa: E402
 
 cfg = vr.CONFIGS[a.config]
 dev = torch.device("cuda", 0)
@@ -40,7 +53,6 @@ W, H = cfg.width, cfg.height
 cam = vr.Camera.reference(W, H)
 lit = vr.setup_constant_values()
 info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
-depth = a.frames_in_flight or (3 if a.config == "C5" else 2)
 B = a.band_rows
 words = vr.band_buffer_words(W, H, B, a.world)
 
@@ -73,17 +85,52 @@ def run(rank, nranks, steps):
     return (time.perf_counter() - t0) / steps * 1e3
 
 
+def lone(rank, nranks, schedule):
+    """One frame alone: render + pack on one stream, HIP events around it, median."""
+    st = torch.cuda.current_stream()
+    buf = pipe.bufs[0]
+
+    def once():
+        vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=B, rank=rank, nranks=nranks,
+                     stream=st, schedule=schedule)
+        if nranks > 1:
+            vr.pack_rgb8(buf[:words], out=packed[0])
+
+    for _ in range(20):
+        once()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(a.latency_reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        once()
+        e1.record(st)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts))
+
+
 single = run(0, 1, a.steps)
+single_lone = {k: lone(0, 1, s) for k, s in (("grid", vr.Schedule.GRID), ("learned", vr.Schedule.HEAVIEST_FIRST))}
 ranks = []
 for r in ([int(x) for x in a.ranks.split(",")] if a.ranks else range(a.world)):
     ms = run(r, a.world, a.steps)
-    ranks.append({"rank": r, "rows": len(owned_rows(H, B, r, a.world)), "ms_per_frame": round(ms, 4)})
+    lg = lone(r, a.world, vr.Schedule.GRID)
+    ll = lone(r, a.world, vr.Schedule.HEAVIEST_FIRST)
+    ranks.append({"rank": r, "rows": len(owned_rows(H, B, r, a.world)), "ms_per_frame": round(ms, 4),
+                  "lone_frame_ms_grid": round(lg, 4), "lone_frame_ms_learned": round(ll, 4)})
     print(json.dumps(ranks[-1]), flush=True)
 slow = max(x["ms_per_frame"] for x in ranks)
+slow_lg = max(x["lone_frame_ms_grid"] for x in ranks)
+slow_ll = max(x["lone_frame_ms_learned"] for x in ranks)
 print(json.dumps({"config": a.config, "width": W, "height": H, "world": a.world, "band_rows": B,
                   "frames_in_flight": depth,
                   "steps": a.steps, "one_gpu_ms_per_frame": round(single, 4),
                   "projected_ms_per_frame": slow, "projected_speedup": round(single / slow, 2),
                   "projected_mrays_per_s": round(W * H / (slow * 1e-3) / 1e6, 1),
+                  "one_gpu_lone_frame_ms": {k: round(v, 4) for k, v in single_lone.items()},
+                  "projected_lone_frame_ms": {"grid": slow_lg, "learned": slow_ll},
+                  "projected_latency_speedup": {"grid": round(single_lone["grid"] / slow_lg, 2),
+                                                "learned": round(single_lone["learned"] / slow_ll, 2)},
                   "note": "max over ranks of each rank's own pipelined frame time on one GPU; RCCL gather not "
                           "included (overlapped with the next frame in bench.py)"}), flush=True)
