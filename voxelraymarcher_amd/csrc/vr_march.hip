@@ -474,6 +474,12 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                         // it reaches bits(64.0f) exactly when iters exceeds kBudget:
                         // one add per iteration.
                         uint32_t ic = this->iters + (0x42800000u - kBudget);
+                        // Every lane's direction in div_fast's domain (nearly every walk): then
+                        // only a cluster-skip plane can give a numerator outside it -- a voxel
+                        // plane (ceilf(o) + EPSILON, floorf(o) - EPSILON) lies >= ~EPSILON/2 from
+                        // o -- so the domain check runs only in wave-iterations where some lane
+                        // skips (a scalar branch; -2 VALU per iteration without a skip).
+                        const bool okw = __builtin_amdgcn_ballot_w64(!walk_ok) == 0;
                         VR_DIAG_COUNT((SHADOW ? 4 : 0) + (SX == 0 ? 1 : 0));   // walk entries
                         for (;;) {
                             VR_DIAG_COUNT((SHADOW ? 6 : 2) + (SX == 0 ? 1 : 0));   // loop iterations
@@ -499,7 +505,8 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                             asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(blk.x), "+v"(blk.y));
                             const bool skip = absent(blk);
                             float nX = vX, nY = vY, nZ = vZ;
-                            if (__builtin_amdgcn_ballot_w64(skip) != 0) {
+                            const bool any_skip = __builtin_amdgcn_ballot_w64(skip) != 0;
+                            if (any_skip) {
                                 float cX = (float)((vx & 0x38) + plane_c8<SX>(cx8)), cY = (float)((vy & 0x38) + plane_c8<SY>(cy8)),
                                       cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
                                 nX = skip ? cX : vX; nY = skip ? cY : vY; nZ = skip ? cZ : vZ;
@@ -512,7 +519,9 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                                   cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
                             asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
                             const bool skip = absent(blk);
+                            const bool any_skip = __builtin_amdgcn_ballot_w64(skip) != 0;
 #endif
+                            const bool chk = !kPos && (!okw || any_skip);   // (uniform)
 #ifdef VR_DIAG
                             {   // wave-iterations where no active lane / every active lane skips a cluster
                                 const uint64_t bs = __builtin_amdgcn_ballot_w64(skip);
@@ -539,25 +548,29 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                                 // a = +0, d < 0), which neither the step nor the crawl test sees
                                 const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
                                 sMin = div_fast(am, rx);
-                                const bool bad = !kPos && !(am >= nlim);
-                                if (!kPos && __builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                                    sMin = bad ? am / fabsf(d.x) : sMin;
-                                    crawl = bad & walk_ok & skip & (sMin == 0.0f) &
-                                            (CRAWL ? ic + 1u - (0x42800000u - kBudget) >= crawl_after : !crawl_off);
-                                    if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
+                                if (chk) {
+                                    const bool bad = !(am >= nlim);
+                                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                                        sMin = bad ? am / fabsf(d.x) : sMin;
+                                        crawl = bad & walk_ok & skip & (sMin == 0.0f) &
+                                                (CRAWL ? ic + 1u - (0x42800000u - kBudget) >= crawl_after : !crawl_off);
+                                        if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
+                                    }
                                 }
                             } else {
                                 float sX = div_fast(ax, rx), sY = div_fast(ay, ry), sZ = div_fast(az, rz);
-                                const bool bad = !kPos && !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
-                                if (!kPos && __builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                                    sX = bad ? (zx ? kInf : ax / d.x) : sX;
-                                    sY = bad ? (zy ? kInf : ay / d.y) : sY;
-                                    sZ = bad ? (zz ? kInf : az / d.z) : sZ;
-                                    // a skip step with t = 0 (its plane axis has n = 0, so it is
-                                    // always on this branch): the ray creeps through an empty cluster
-                                    crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
-                                            (CRAWL ? ic + 1u - (0x42800000u - kBudget) >= crawl_after : !crawl_off);
-                                    if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
+                                if (chk) {
+                                    const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
+                                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                                        sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                                        sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                                        sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                                        // a skip step with t = 0 (its plane axis has n = 0, so it is
+                                        // always on this branch): the ray creeps through an empty cluster
+                                        crawl = bad & walk_ok & skip & (fminf(sX, fminf(sY, sZ)) == 0.0f) &
+                                                (CRAWL ? ic + 1u - (0x42800000u - kBudget) >= crawl_after : !crawl_off);
+                                        if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
+                                    }
                                 }
                                 sMin = fminf(sX, fminf(sY, sZ));
                                 const bool vox = !skip && !found;        // a voxel step: its t values feed the normal
@@ -710,6 +723,9 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             const float ex = gx * kEps, ey = gy * kEps, ez = gz * kEps;
             const bool walk_ok = rx.ok && ry.ok && rz.ok && !zx && !zy && !zz;
             const float nlim = walk_ok ? 0x1p-90f : kInf;
+            // no cluster skips here: with every lane's direction in div_fast's domain no
+            // numerator (a voxel plane's, >= ~EPSILON/2 from o) leaves it -- no check at all
+            const bool okw = __builtin_amdgcn_ballot_w64(!walk_ok) == 0;
             uint32_t key = 0;
             uint2 e1{0u, 0u}, e2{0u, 0u};
             uint32_t ic = this->iters + (0x42800000u - kBudget);   // biased count (see the VCS walk)
@@ -725,15 +741,19 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                 if (EQ) {                                 // see grid_original
                     const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
                     sMin = div_fast(am, rx);
-                    const bool bad = !(am >= nlim);
-                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) sMin = bad ? am / fabsf(d.x) : sMin;
+                    if (!okw) {
+                        const bool bad = !(am >= nlim);
+                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) sMin = bad ? am / fabsf(d.x) : sMin;
+                    }
                 } else {
                     sX = div_fast(ax, rx); sY = div_fast(ay, ry); sZ = div_fast(az, rz);
-                    const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
-                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                        sX = bad ? (zx ? kInf : ax / d.x) : sX;
-                        sY = bad ? (zy ? kInf : ay / d.y) : sY;
-                        sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                    if (!okw) {
+                        const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
+                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                            sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                            sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                            sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                        }
                     }
                     sMin = fminf(sX, fminf(sY, sZ));
                 }
