@@ -330,6 +330,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pipe.step(render)
+    t_enq = time.perf_counter() - t0            # host time to enqueue every frame
     pipe.drain()
     torch.cuda.synchronize()
     barrier()
@@ -437,6 +438,7 @@ def main():
                                "groups first, learned from earlier launches of the same view), kernel_ms_grid_order "
                                "in grid order (a first render)",
             "kernel_mrays_per_s": round(W * H / world / (kern_grid_ms * 1e-3) / 1e6, 2),
+            "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "roofline": roof,
             # the non-instrumented launches of this run in order, per phase (a rocprofv3 kernel
             # trace of the same command splits into them: profiles/roofline_phases.py)
