@@ -1646,7 +1646,9 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, ALGO == ALGO_ORIGINAL ? VR_
     const uint32_t l = (by * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
     uint32_t bytes = 0, iters = 0;
     if (x < v.W && l < v.local_rows) {
-        v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes, v.cost ? &iters : nullptr);
+        // (&iters unconditionally: a pointer chosen by `v.cost ? &iters : nullptr` keeps
+        // iters in scratch -- a store and a reload per lane, 8 MB of WRITE_SIZE per C2 launch)
+        v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes, &iters);
     }
     if (COUNT) add_bytes(v, lane, bytes);
     if (v.cost) {                                  // the wave's walk length, for the next work order
