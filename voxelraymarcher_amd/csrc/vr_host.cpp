@@ -693,9 +693,11 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // stream-ordered allocations.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) heavy = false;
-    // crawl records per wave: a lone frame ends with the crawl pass's longest chain (4 per
-    // wave); with frames in flight the pass's issue cycles are what count (8 per wave)
-    v.crawl_rpw = crawl_rpw_override() ? crawl_rpw_override() : (alone ? 4u : 8u);
+    // crawl records per wave: a lone frame ends with the crawl pass's longest chain (2 per
+    // wave since round 4's shorter chains: C5 alone 0.767 -> 0.759 ms vs 4,
+    // profiles/r04/crawl/scene_lds_ab.txt, rpw_multi_cluster.txt); with frames in flight the
+    // pass's issue cycles are what count (8 per wave)
+    v.crawl_rpw = crawl_rpw_override() ? crawl_rpw_override() : (alone ? 2u : 8u);
     D.any = true;
     D.last_stream = st;
     D.last_idx = lease.idx;
