@@ -19,12 +19,21 @@ k's gather runs beside frame k+1's render.  Every frame is still rendered in ful
 Inputs (scene, camera) are resident in HBM before timing starts; the timed region
 ends after the last frame's gather and assembly.  Rank 0 prints ONE JSON line.
 
-`value`/`ms_per_step` are the pipelined throughput; `kernel_ms` is one launch
-timed alone (HIP events on the launch stream, nothing overlapping).
+`value`/`ms_per_step` are the pipelined throughput; `kernel_ms` (learned work order)
+and `kernel_ms_grid_order` (a first render's grid order) are one launch timed alone:
+one pair of HIP events around 200 isolated launches on the launch stream.
 
-roofline: `achieved`/`frac` are the north star's figure -- the algorithmic bytes
-of one launch (the words the reference walk reads, counted by the
-instrumented kernel) / that launch's average duration `kernel_ms` / 8 TB/s.
+roofline: `achieved`/`frac` are the north star's figure for ONE launch in grid order --
+the algorithmic bytes the launch issues (the words the reference walk
+reads, counted by the instrumented kernel, minus the existence reads of the crawl
+iterations the crawl pass fast-forwards in closed form and never loads:
+`algorithmic_bytes_issued_per_launch`, `crawl_iterations_fast_forwarded`) /
+`kernel_ms_grid_order` / 8 TB/s.  `frac_learned_order` uses `kernel_ms`,
+`frac_pipelined` `ms_per_step` (C2 reaches ~1.0 there: its counted 4-B words are
+answered by 8-B mask-record loads that mostly hit the vector L1 -- DESIGN.md 6),
+`frac_section8d` the unreduced 8(d) bytes.  `dispatch_phases` lists the run's
+launch phases in order, so that profiles/roofline_phases.py can recompute every
+fraction from a rocprofv3 kernel trace of the same command.
 `bound` is the MEASURED limiter, from the round's PMC profile
 (profiles/traffic.json, keyed by config, written by profiles/collect_traffic.py):
 "valu" when the walk's VALU issue is closer to its roof than the measured HBM
