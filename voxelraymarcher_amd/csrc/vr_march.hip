@@ -974,38 +974,13 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                                                      bool& tail, uint32_t& hcol, uint32_t& hcode) {
         const float dL = ax3<PL>(ds), dM = ax3<PM>(ds), dS = ax3<PS>(ds);
         auto dv = [](float n, float d) { return UNIT ? n * d : n / d; };
-        // VR_LONG_FAST_DIV: n / d by div_fast with the reciprocal made right here from a
-        // pinned copy of d (an empty asm on it: never hoisted into a loop-carried VGPR, the
-        // spill growth that sank every hoisted-reciprocal variant), IEEE division for lanes
-        // outside div_fast's domain (one ballot).  Numerators here are never -0 (x - x = +0).
-#ifndef VR_LONG_FAST_DIV
-#define VR_LONG_FAST_DIV 0
-#endif
+        // (IEEE divisions here: div_fast with reciprocals made at each use, pinned so they
+        // are never loop-carried, measured slower -- C3 0.2264 -> 0.2358 ms per frame,
+        // profiles/r04/ab_lfd_rolled.txt -- as every hoisted-reciprocal variant before it)
         auto dv3 = [&](float n0, float d0, float n1, float d1, float n2, float d2, float& q0, float& q1, float& q2) {
-            if (UNIT || !VR_LONG_FAST_DIV) {
-                q0 = dv(n0, d0); q1 = dv(n1, d1); q2 = dv(n2, d2);
-                return;
-            }
-            float e0 = d0, e1 = d1, e2 = d2;
-            asm volatile("" : "+v"(e0), "+v"(e1), "+v"(e2));
-            const Rcp r0 = rcp_setup(e0), r1 = rcp_setup(e1), r2 = rcp_setup(e2);
-            q0 = div_fast(n0, r0); q1 = div_fast(n1, r1); q2 = div_fast(n2, r2);
-            auto ok = [](float n, const Rcp& r) { return __float_as_uint(n) == 0u || div_fast_ok(n, r); };
-            const bool good = ok(n0, r0) && ok(n1, r1) && ok(n2, r2);
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(!good) != 0, 0)) {
-                q0 = good ? q0 : n0 / d0; q1 = good ? q1 : n1 / d1; q2 = good ? q2 : n2 / d2;
-            }
+            q0 = dv(n0, d0); q1 = dv(n1, d1); q2 = dv(n2, d2);
         };
-        auto dv1 = [&](float n, float d) {
-            if (UNIT || !VR_LONG_FAST_DIV) return dv(n, d);
-            float e = d;
-            asm volatile("" : "+v"(e));
-            const Rcp r = rcp_setup(e);
-            float q = div_fast(n, r);
-            const bool good = __float_as_uint(n) == 0u || div_fast_ok(n, r);
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(!good) != 0, 0)) q = good ? q : n / d;
-            return q;
-        };
+        auto dv1 = [&](float n, float d) { return dv(n, d); };
         const bool posL = (cls >> (2 * PL)) & 1u, posM = (cls >> (2 * PM)) & 1u, posS = (cls >> (2 * PS)) & 1u;
         const bool negL = (cls >> (2 * PL + 1)) & 1u, negM = (cls >> (2 * PM + 1)) & 1u;
         const int32_t offL = posL ? 8 : 0, offM = posM ? 8 : 0, offS = posS ? 8 : 0;
