@@ -172,6 +172,9 @@ class BandGather:
             self.on_frame(f.view(self.H, self.W, 3) if self.rgb8 else f)
 
     def _finish(self, slot: int) -> None:
+        if self.R == 1 and self.on_frame is None:     # nothing to hand over (the bench's loop)
+            self.pending.remove(slot)
+            return
         with self._slot_stream(slot):
             if self.R == 1:
                 if self.on_frame is not None:
