@@ -169,7 +169,9 @@ __device__ __forceinline__ bool absent(Blk b) { return b.y == kNone; }
 
 struct Hit {
     uint32_t col;       // the voxel's stored colour
-    f3 n;               // surface normal for the lighting
+    uint32_t nc;        // surface normal for the lighting: one component +-1, the others +0
+                        // (every normal the walks make), as bits(+-1.0f) | axis -- one VGPR
+                        // instead of three across the lighting (see normal_of)
     f3 so;              // hit location (region-local): lighting point and shadow-ray origin
     i3 region;          // currentRegion at the hit
     bool longest;       // isInShadowRayMarchVoxelSceneLongestAxis vs ...Original
@@ -380,7 +382,8 @@ struct Ctx {
 
     // applyLighting / applyDirectionalLightingToColor / applyPointLightingToColor
     // (Renderer.cuh:57-86,249-258), colour packing (VoxelFunctions.cuh:69-83).
-    __device__ __forceinline__ uint32_t lighting(uint32_t col, f3 n, f3 rwp, f3 ro) const {
+    __device__ __forceinline__ uint32_t lighting(uint32_t col, uint32_t nc, f3 rwp, f3 ro) const {
+        const f3 n = normal_of(nc);
         f3 LC = ld3(v.LC);
         // convertRGBIntegerColorToVector: c / 255.0f per channel, correctly rounded
         // (div255); colours are < 2^24 so R = col >> 16 <= 255.
@@ -411,10 +414,20 @@ struct Ctx {
     }
 
     // getNormalFromTValues (Renderer.cuh:237-247)
-    __device__ __forceinline__ static f3 normal_from_t(float tX, float tY, float tZ, float tMin, f3 d) {
-        if (tX == tMin) return mk(neg_sign_one(d.x), 0.0f, 0.0f);
-        if (tY == tMin) return mk(0.0f, neg_sign_one(d.y), 0.0f);
-        return mk(0.0f, 0.0f, neg_sign_one(d.z));
+    __device__ __forceinline__ static uint32_t normal_from_t(float tX, float tY, float tZ, float tMin, f3 d) {
+        if (tX == tMin) return ncode(0u, neg_sign_one(d.x));
+        if (tY == tMin) return ncode(1u, neg_sign_one(d.y));
+        return ncode(2u, neg_sign_one(d.z));
+    }
+    // Hit::nc: the normal whose component `axis` is `one` (+-1.0f, low mantissa bits 0)
+    // and whose other components are +0.0f
+    __device__ __forceinline__ static uint32_t ncode(uint32_t axis, float one) {
+        return __float_as_uint(one) | axis;
+    }
+    __device__ __forceinline__ static f3 normal_of(uint32_t nc) {
+        const float one = __uint_as_float(nc & ~3u);
+        const uint32_t a = nc & 3u;
+        return mk(a == 0u ? one : 0.0f, a == 1u ? one : 0.0f, a == 2u ? one : 0.0f);
     }
 
     __device__ __forceinline__ static bool in_region(f3 o) {               // Renderer.cuh:93-98

@@ -787,7 +787,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             h.col = col;
             // tMin is always min(tX, tY, tZ) of the same step: recomputed here
             // instead of carried through the loop
-            h.n = normal_from_t(tX, tY, tZ, fminf(tX, fminf(tY, tZ)), d);
+            h.nc = normal_from_t(tX, tY, tZ, fminf(tX, fminf(tY, tZ)), d);
             h.so = o;
             h.region = cr;
             h.longest = false;
@@ -880,12 +880,10 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                     h.region = cr;
                     h.longest = true;
                     if (jumping) {                   // performVoxelSpaceJump's hit
-                        h.n = normal_from_t(tX, tY, tZ, tMin, ds);
+                        h.nc = normal_from_t(tX, tY, tZ, tMin, ds);
                         h.so = old_o;
                     } else {                         // an axis step's hit
-                        f3 n = mk(0.0f, 0.0f, 0.0f);
-                        setf(n, axis, copysignf(1.0f, -comp(ds, axis)));
-                        h.n = n;
+                        h.nc = this->ncode(axis, copysignf(1.0f, -comp(ds, axis)));
                         if (axis == L) {
                             h.so = ray_o;
                         } else {                     // getLocalHitLocation (Renderer.cuh:753-758)
@@ -1296,7 +1294,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             const float one = (hcode & 4u) ? 1.0f : -1.0f;
             const uint32_t a = hcode & 3u;
             h.col = hcol;
-            h.n = mk(a == 0u ? one : 0.0f, a == 1u ? one : 0.0f, a == 2u ? one : 0.0f);
+            h.nc = this->ncode(a, one);
             h.so = oo;
             h.region = cr;
             h.longest = true;
@@ -1466,7 +1464,7 @@ __device__ __forceinline__ uint32_t light_and_shadow(Walker<STORE, COUNT, CRAWL>
     bool sh = false;
     const f3 rwp = add(ld3(v.translation), mk((float)(h.region.x * kBlock), (float)(h.region.y * kBlock),
                                               (float)(h.region.z * kBlock)));
-    const uint32_t lit = w.lighting(h.col, h.n, rwp, h.so);
+    const uint32_t lit = w.lighting(h.col, h.nc, rwp, h.so);
     if (v.use_shadows) {
         VR_DIAG_COUNT(16);                             // shadow walks started
         w.lit_saved = lit;
