@@ -650,6 +650,14 @@ bool crawl_scene_lds_enabled() {
     }();
     return on;
 }
+// VR_INFLIGHT_WAVES=0 (A/B runs): frames in flight keep the lone-frame occupancy.
+bool in_flight_occupancy() {
+    static const bool on = [] {
+        const char* e = std::getenv("VR_INFLIGHT_WAVES");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 bool order_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("VR_ORDER");
@@ -735,7 +743,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
                             ? 1u : 0u;
     const uint32_t cwgs = v.crawl_scene_lds ? vr::crawl_grid_scene_lds(expect, v.crawl_rpw)
                                             : vr::crawl_grid(expect, v.crawl_rpw);
-    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs);
+    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs, !alone && in_flight_occupancy());
     if (e == hipSuccess && remake) {
         // (on a side stream instead -- one more stream than the box's 4 hardware queues
         // serialised the two render streams: C2 0.1124 -> 0.1277 ms per frame in flight,

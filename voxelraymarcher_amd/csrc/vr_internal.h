@@ -134,8 +134,10 @@ constexpr uint32_t kDeferWords = 4 + kDeferCap * kDeferRecWords;
 
 // Launch one render (defined in vr_march.hip): the tile pass and the crawl pass on
 // `stream`, the crawl pass with `crawl_wgs` workgroups (any number is correct).
+// in_flight: another stream's launch is still running on the device (the tile pass then
+// takes its higher-occupancy variant where one exists, vr_march.hip TileWaves)
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,
-                        hipStream_t stream, uint32_t crawl_wgs);
+                        hipStream_t stream, uint32_t crawl_wgs, bool in_flight);
 // Crawl-pass grid for a launch that expects about `records` deferred pixels.
 uint32_t crawl_grid(uint32_t records, uint32_t rpw);
 // The crawl pass's shape (vr_march.hip): threads per workgroup and dynamic LDS bytes for the

@@ -1609,9 +1609,25 @@ __device__ __forceinline__ void add_ff(const KView& v, uint32_t lane, unsigned l
 #ifndef VR_LONG_WAVES
 #define VR_LONG_WAVES 6
 #endif
+// HI: the occupancy for frames in flight, where the other frame's waves fill the tail and
+// the pass's throughput counts: one wave per SIMD more for the cuckoo walk (latency-bound
+// on its random slot loads: C4 0.0861 -> 0.0855 ms per frame, but 0.1229 -> 0.1246 alone)
+// and the longest-axis walk (C3 0.2311 -> 0.2289 per frame, 0.2815 -> 0.2862 alone),
+// profiles/r04/ab_orig_waves_C4.txt, ab_long_waves_C3.txt.  The host picks HI for a launch
+// whose device is still running another stream's (the AUTO schedule's test).
+#ifndef VR_ORIG_WAVES_HI
+#define VR_ORIG_WAVES_HI 8
+#endif
+#ifndef VR_LONG_WAVES_HI
+#define VR_LONG_WAVES_HI 7
+#endif
+template <int ALGO, bool HI> struct TileWaves {
+    static constexpr int value = ALGO == ALGO_ORIGINAL ? (HI ? VR_ORIG_WAVES_HI : VR_ORIG_WAVES)
+                                                       : (HI ? VR_LONG_WAVES_HI : VR_LONG_WAVES);
+};
 static_assert(kTilesX * kTilesY == kWavesPerTileGroup, "cost layout (vr_internal.h)");
-template <int STORE, int ALGO, bool COUNT>
-__global__ __launch_bounds__(64 * kTilesX * kTilesY, ALGO == ALGO_ORIGINAL ? VR_ORIG_WAVES : VR_LONG_WAVES) void march_kernel(KScene s, KView v) {
+template <int STORE, int ALGO, bool COUNT, bool HI = false>
+__global__ __launch_bounds__(64 * kTilesX * kTilesY, (TileWaves<ALGO, HI>::value)) void march_kernel(KScene s, KView v) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t bx, by;
     tile_group(v, bx, by);
@@ -1873,7 +1889,7 @@ hipError_t launch_order(const uint32_t* cost, uint32_t n, uint32_t columns, uint
 }
 
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream,
-                        uint32_t crawl_wgs) {
+                        uint32_t crawl_wgs, bool in_flight) {
     uint32_t gx, gy;
     march_grid(v, gx, gy);
     dim3 grid(gx, gy);
@@ -1883,9 +1899,10 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
     const bool scene_lds = v.crawl_scene_lds != 0;
     const dim3 cblock(crawl_threads(scene_lds));
     const uint32_t clds = crawl_lds_bytes(s, scene_lds);
-#define VR_LAUNCH(ST, AL, CT)                                                                     \
+#define VR_LAUNCH(ST, AL, CT) VR_LAUNCH_HI(ST, AL, CT, false)
+#define VR_LAUNCH_HI(ST, AL, CT, HI)                                                              \
     do {                                                                                           \
-        hipLaunchKernelGGL((march_kernel<ST, AL, CT>), grid, block, 0, stream, s, v);              \
+        hipLaunchKernelGGL((march_kernel<ST, AL, CT, HI>), grid, block, 0, stream, s, v);          \
         if (v.defer && !kNoCrawlPass) {                                                            \
             static const hipError_t attr = hipFuncSetAttribute(                                    \
                 reinterpret_cast<const void*>(&crawl_kernel<ST, AL, CT>),                          \
@@ -1901,14 +1918,23 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
     VR_LAUNCH(STORE_VCS, VR_ISA_ONLY, false);
     return hipGetLastError();
 #endif
+    // (the in-flight occupancy variants exist for the uninstrumented cuckoo original and
+    // VCS longest-axis walks; the VCS original walk is fastest at 7 waves either way)
+    const bool hi = in_flight && !count;
     if (store == STORE_VCS) {
         if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, false); }
+        else if (hi) VR_LAUNCH_HI(STORE_VCS, ALGO_LONGEST, false, true);
         else { if (count) VR_LAUNCH(STORE_VCS, ALGO_LONGEST, true); else VR_LAUNCH(STORE_VCS, ALGO_LONGEST, false); }
     } else {
-        if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_HASH, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_HASH, ALGO_ORIGINAL, false); }
+        if (algo == ALGO_ORIGINAL) {
+            if (hi) VR_LAUNCH_HI(STORE_HASH, ALGO_ORIGINAL, false, true);
+            else if (count) VR_LAUNCH(STORE_HASH, ALGO_ORIGINAL, true);
+            else VR_LAUNCH(STORE_HASH, ALGO_ORIGINAL, false);
+        }
         else { if (count) VR_LAUNCH(STORE_HASH, ALGO_LONGEST, true); else VR_LAUNCH(STORE_HASH, ALGO_LONGEST, false); }
     }
 #undef VR_LAUNCH
+#undef VR_LAUNCH_HI
     return hipGetLastError();
 }
 
