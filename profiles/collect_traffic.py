@@ -12,6 +12,7 @@
   clock: GRBM_GUI_ACTIVE (sums the 8 XCDs) over the rocprof kernel duration.
   python3 profiles/collect_traffic.py <profile dir> <config> [merge_into.json]"""
 import csv
+import re
 import glob
 import json
 import os
@@ -26,7 +27,7 @@ def per_dispatch(d, counter):
             n = r["Kernel_Name"]
             if r["Counter_Name"] != counter or "march_kernel" not in n:
                 continue
-            if "true>" in n:          # the COUNT instantiation (bytes counter), not the timed kernel
+            if re.search(r"kernel<\d+, \d+, true[,>]", n):   # the COUNT instantiation (bytes counter)
                 continue
             vals.setdefault(n, []).append(float(r["Counter_Value"]))
     return vals

@@ -6,7 +6,7 @@ recompute every roofline fraction of its JSON line from the trace alone.
 
 bench.py prints `dispatch_phases` -- the number of non-instrumented launches per phase, in
 submission order: warmup, untimed, iso_grid, iso_learned, latency (N > 1), timed.  Every
-launch is one tile-pass dispatch (`march_kernel<S, A, false>`) followed by one crawl-pass
+launch is one tile-pass dispatch (`march_kernel<S, A, false[, HI]>`) followed by one crawl-pass
 dispatch (`crawl_kernel<S, A, false>`) on the same stream, sometimes plus a work-order build
 (`order_kernel`, every 16th heaviest-first launch of a slot).  Dispatches are taken in
 Dispatch_Id order (submission order); the instrumented launch (`<..., true>`) is not counted.
@@ -57,7 +57,7 @@ def main():
             continue
         kind = ("tile" if "march_kernel" in name else "crawl" if "crawl_kernel" in name else
                 "order" if "order_kernel" in name else None)
-        if kind is None or re.search(r"kernel<\d+, \d+, true>", name):
+        if kind is None or re.search(r"kernel<\d+, \d+, true[,>]", name):
             continue
         rows.append((int(r["Dispatch_Id"]), kind, name, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     rows.sort()
