@@ -6,9 +6,12 @@ roofline of the dominant kernel and the CPU oracle baseline.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
                   [--tiling auto|weak|fixed]
 
-A step = one full frame.  The frame's rows are cut into interleaved 8-row bands
-(band b -> rank b % N); each rank renders its bands and every frame is gathered to
-rank 0 over RCCL as RGB8 (3 B per pixel) and assembled there.  Tiling:
+A step = one full frame.  With N > 1 ranks the frame is dealt over the ranks --
+fixed tiling: the 2-D tile deal (every 8-row band cut into 16-column blocks, block j
+of band b -> rank (j + 3b) % N, so expensive rows are spread over every rank; --layout
+bands keeps whole 8-row bands, band b -> rank b % N); weak tiling: 8-row bands -- each
+rank renders its share and every frame is gathered to rank 0 over RCCL as RGB8 (3 B
+per pixel) and assembled there.  Tiling:
   fixed -- the config's own frame whatever N is (strong scaling; BASELINE C5 is
            defined this way: one 3840x2160 frame tiled over 8 GPUs);
   weak  -- the same view at about N x the pixels (each side x sqrt(N));
@@ -85,6 +88,13 @@ def parse():
                    help="every rank on cuda:0 (rehearse N ranks on a one-GPU box; needs --backend gloo)")
     p.add_argument("--resolution", default="",
                    help="WxH instead of the config's frame (tests; the same view and scene)")
+    p.add_argument("--layout", default="auto", choices=["auto", "bands", "tiles"],
+                   help="how the frame is dealt over N > 1 ranks: 8-row bands, or the 2-D tile deal (8-row bands "
+                        "cut into --tile-cols column blocks); auto = tiles for fixed tiling, bands for weak")
+    p.add_argument("--tile-cols", type=int, default=16, help="column block of the 2-D tile deal (one workgroup)")
+    p.add_argument("--exchange", action="store_true",
+                   help="run the N > 1 frame exchange (process group, RGB8 pack, gather, rank-0 assembly) even "
+                        "with one rank: exercises the RCCL calls on a one-GPU box")
     p.add_argument("--dump-frame", default="",
                    help="rank 0 saves the last frame of the timed loop (.npy): RGB8 [H, W, 3] with N > 1 ranks, "
                         "packed 0x00RRGGBB words [H, W] with one")
@@ -102,7 +112,8 @@ if ARGS is not None:
     # ranks sharing one GPU (--same-device) keep the default: their queues add up on one device)
     _q = ARGS.hw_queues or (0 if ARGS.same_device else
                             pipeline_hw_queues(ARGS.frames_in_flight or pipeline_depth(ARGS.config),
-                                               int(os.environ.get("WORLD_SIZE", "1"))))
+                                               max(int(os.environ.get("WORLD_SIZE", "1")),
+                                                   2 if ARGS.exchange else 1)))
     _have = os.environ.get("GPU_MAX_HW_QUEUES", "")
     if _q and (ARGS.hw_queues or not _have.isdigit() or int(_have) < _q):
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(int(_q), 16))
@@ -232,17 +243,18 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    dev, backend, stage_host = init_frame_group(world, local, args.backend, args.same_device)
+    grouped = world > 1 or args.exchange
+    dev, backend, stage_host = init_frame_group(world, local, args.backend, args.same_device, force_group=grouped)
 
     def allreduce(x: float | int, op=dist.ReduceOp.SUM, dtype=torch.float64):
         """A scalar over the ranks (host tensors for gloo, device tensors for RCCL)."""
         t = torch.tensor([x], dtype=dtype, device="cpu" if stage_host else dev)
-        if world > 1:
+        if grouped:
             dist.all_reduce(t, op=op)
         return t.item()
 
     def barrier():
-        if world > 1:
+        if grouped:
             dist.barrier()
 
     cfg = vr.CONFIGS[args.config]
@@ -258,10 +270,16 @@ def main():
     # N > 1: bands travel as the RGB8 framebuffer (writeColorToFramebuffer's format, 3 B per
     # pixel): rank 0 ends each frame with the RGB8 image
     depth = args.frames_in_flight or pipeline_depth(args.config)
-    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=depth, rgb8=world > 1, stage_host=stage_host)
+    layout = args.layout if args.layout != "auto" else ("tiles" if tiling == "fixed" else "bands")
+    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=depth, rgb8=grouped, stage_host=stage_host,
+                      tile_cols=args.tile_cols if layout == "tiles" else 0, exchange=grouped)
+    tcols = pipe.T          # 0: row bands (every N = 1 run without --exchange)
 
     def render(buf):   # on the current stream (BandGather's slot stream in the loops)
-        vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, rank, world, buf)
+        if tcols:
+            vr.render_tiles(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, tcols, rank, world, buf)
+        else:
+            vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, rank, world, buf)
 
     # algorithmic bytes of THIS rank's launch (its bands; instrumented kernel,
     # untimed) and of the whole frame (sum over ranks); `stats`: the part of
@@ -270,7 +288,7 @@ def main():
     ctr = torch.zeros(1, dtype=torch.int64, device=dev)
     stats = torch.zeros(2, dtype=torch.int64, device=dev)
     vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, pipe.bufs[0], band_rows=BAND_ROWS, rank=rank,
-                 nranks=world, counter=ctr, stats=stats)
+                 nranks=world, counter=ctr, stats=stats, tile_cols=tcols)
     torch.cuda.synchronize()
     launch_bytes = int(ctr.item())
     ff_iters, ff_bytes = (int(x) for x in stats.cpu().tolist())
@@ -303,7 +321,7 @@ def main():
 
     def render_grid(buf):
         vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=BAND_ROWS, rank=rank, nranks=world,
-                     stream=stream, schedule=vr.Schedule.GRID)
+                     stream=stream, schedule=vr.Schedule.GRID, tile_cols=tcols)
 
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     ev_grid = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -322,7 +340,7 @@ def main():
     # N > 1: latency of ONE frame, first launch -> gathered and assembled on
     # rank 0, without the overlap of the pipelined loop
     frame_latency_ms = None
-    if world > 1:
+    if grouped:
         lat = []
         for _ in range(5):
             barrier()
@@ -418,8 +436,9 @@ def main():
              f"achieved HBM GB/s")
         gather = ("RCCL gather" if backend == "nccl" else "gloo gather staged through host memory") + \
             (" (ranks sharing cuda:0)" if args.same_device else "")
-        par = f"row-band tiles x{world}" + (f" + {gather} of the RGB8 bands to rank 0 (overlapped with the "
-                                             "next frame)" if world > 1 else "")
+        deal = (f"2-D tile deal x{world} (8x{tcols} blocks, block j of 8-row band b -> rank (j + "
+                f"{pipe.stride}b) % {world})" if tcols else f"row-band tiles x{world}")
+        par = deal + (f" + {gather} of the RGB8 tiles to rank 0 (overlapped with the next frame)" if grouped else "")
         line = {
             "metric": metric,
             "value": round(mrays, 2),
@@ -438,7 +457,8 @@ def main():
                                                                        f"scaling)"),
                        "grid": cfg.grid, "width": W, "height": H, "tiling": tiling,
                        "store": cfg.store.name, "algorithm": cfg.algorithm.name, "scale": cfg.scale,
-                       "voxels": int(len(rgb)), "parallelism": par, "frames_in_flight": pipe.depth,
+                       "voxels": int(len(rgb)), "parallelism": par, "layout": "tiles" if tcols else "bands",
+                       "frames_in_flight": pipe.depth,
                        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default")},
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_grid_order": round(kern_grid_ms, 4),
@@ -452,7 +472,7 @@ def main():
             # the non-instrumented launches of this run in order, per phase (a rocprofv3 kernel
             # trace of the same command splits into them: profiles/roofline_phases.py)
             "dispatch_phases": {"warmup": args.warmup, "untimed": 40, "iso_grid": n_iso, "iso_learned": n_iso,
-                                "latency": 5 if world > 1 else 0, "timed": args.steps},
+                                "latency": 5 if grouped else 0, "timed": args.steps},
         }
         if HW_QUEUES_REQUESTED is not None:
             line["config"]["hw_queues_requested"] = HW_QUEUES_REQUESTED
@@ -461,7 +481,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, xyz, rgb, args.cpu_threads or baseline_threads())
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

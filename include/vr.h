@@ -151,6 +151,28 @@ int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const
 /* Number of uint32 words vr_render_bands writes per rank. */
 uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t nranks);
 
+/* The 2-D tile deal (vr_render_opts.tile_cols): every band_rows-row band of the frame is
+ * cut into column blocks of tile_cols pixels, block j of band b -> rank (j + stride*b) %
+ * nranks.  Row bands alone put a cluster of expensive rows (C5's crawl rows) on one or two
+ * ranks; the deal gives every rank a share of every band while each 8x8 wave tile stays
+ * whole.  out_dev: vr_tile_buffer_words(...) uint32 per rank (same for every rank). */
+int vr_render_tiles(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
+                    const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
+                    uint32_t band_rows, uint32_t tile_cols, uint32_t rank, uint32_t nranks,
+                    uint32_t* out_dev, void* stream);
+uint64_t vr_tile_buffer_words(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t tile_cols,
+                              uint32_t nranks);
+/* The stride the deal uses when deal_stride is 0: 3 (a knight's-move deal) unless it
+ * shares a factor with nranks, else 1. */
+uint32_t vr_deal_stride_default(uint32_t nranks);
+/* Rank 0's reassembly after the gather: parts_dev holds the nranks tile buffers back to
+ * back (each vr_tile_buffer_words(...) pixels of elem_bytes bytes: 4 for the packed words,
+ * 3 for RGB8), frame_dev receives the width x height image (row-major, elem_bytes per
+ * pixel).  deal_stride 0 = the default.  Asynchronous on `stream`. */
+int vr_assemble_tiles(const void* parts_dev, void* frame_dev, uint32_t elem_bytes, uint32_t width,
+                      uint32_t height, uint32_t band_rows, uint32_t tile_cols, uint32_t nranks,
+                      uint32_t deal_stride, void* stream);
+
 /* Kernel implementations behind vr_render*: all produce identical pixels.
  * (Value 2 was a persistent state-machine kernel, retired in round 3: it was
  * never the fastest; it is rejected with VR_E_INVALID.) */
@@ -188,15 +210,42 @@ typedef struct {
     /* (optional, device uint64[2], caller-zeroed; read only with bytes_dev) the part of
      * bytes_dev's count that the kernels credit without loading it: [0] cluster-skip crawl
      * iterations fast-forwarded in closed form (Renderer.cuh:290-306, performVoxelSpaceJump
-     * :707-725), [1] their existence-read bytes (4 each).  bytes_dev - [1] = the bytes the
-     * walk's own reads stand for. */
+     * :707-725), [1] the existence-read bytes credited without a load -- 4 per fast-forwarded
+     * iteration and 4 per crawl-pass skip step answered from its LDS copy of the region's
+     * cluster-existence bits.  bytes_dev - [1] = the bytes the kernels' own loads stand for. */
     uint64_t* stats_dev;
+    /* (round 5) vr_occupancy: which occupancy variant of the tile pass renders.  The
+     * uninstrumented cuckoo `original` and VCS `longestaxis` walks have a higher-occupancy
+     * variant for frames in flight; AUTO takes it when another stream's launch is still
+     * running on the device.  Pixels never depend on it.  Instrumented launches (bytes_dev)
+     * always run the lone variant. */
+    uint32_t occupancy;
+    /* (round 5) 2-D tile deal.  0: bands of whole rows, band b -> rank b % nranks (the layout
+     * described at vr_render_bands).  > 0: the rows [row_begin,row_end) are cut into bands of
+     * band_rows rows (0 = one band) and every band into column blocks of tile_cols pixels; block
+     * j of band b belongs to rank (j + stride * b) % nranks, stride = deal_stride (0 =
+     * vr_deal_stride_default(nranks)).  out_dev then holds, for every band in order, this rank's
+     * blocks of that band in increasing j, each band_rows x tile_cols, as rows of
+     * ceil(ceil(width/tile_cols)/nranks) * tile_cols words (vr_tile_buffer_words); pixels past
+     * the frame are written as 0.  Every rank gets a share of every band, so expensive rows
+     * (long walks are spatially clustered) are spread over all ranks. */
+    uint32_t tile_cols;
+    uint32_t deal_stride;
+    uint32_t reserved2;   /* 0 */
 } vr_render_opts;
 /* The smallest struct_size accepted: the layout up to and including `reserved`. */
 #define VR_RENDER_OPTS_MIN_SIZE 48u
 
+typedef enum {
+    VR_OCCUPANCY_AUTO = 0,
+    VR_OCCUPANCY_LONE = 1,        /* the lone-frame variant (7 waves/SIMD original, 6 longest axis) */
+    VR_OCCUPANCY_IN_FLIGHT = 2    /* the frames-in-flight variant where one exists (cuckoo original 8,
+                                     VCS longest axis 7) */
+} vr_occupancy;
+
 /* Defaults: struct_size = sizeof(vr_render_opts), kernel AUTO, rows [0, UINT32_MAX) --
- * clipped to the frame by the render call -- one band, rank 0 of 1, schedule AUTO. */
+ * clipped to the frame by the render call -- one band, rank 0 of 1, schedule AUTO,
+ * occupancy AUTO, no tile deal. */
 int vr_render_opts_init(vr_render_opts* opts);
 
 /* Work order of the tile pass.  A frame's time alone is set by its slowest tiles:
@@ -212,6 +261,9 @@ typedef enum {
     VR_SCHEDULE_GRID = 1,
     VR_SCHEDULE_HEAVIEST_FIRST = 2
 } vr_schedule;
+/* Every vr_render* call returns VR_E_INVALID on a stream that is capturing a HIP graph
+ * (its per-device slot ring and work-order bookkeeping are host state that a graph replay
+ * would not repeat). */
 int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
                  const float translation[3], uint32_t scale, uint32_t width, uint32_t height,
                  const vr_render_opts* opts, uint32_t* out_dev, void* stream);

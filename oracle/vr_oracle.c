@@ -378,6 +378,19 @@ static inline int same_v(v3f a, v3f b) { return same_f(a.v[0], b.v[0]) && same_f
 static inline int same_i(v3i a, v3i b) { return a.v[0] == b.v[0] && a.v[1] == b.v[1] && a.v[2] == b.v[2]; }
 /* The loop would repeat this iteration forever: give up on the pixel. */
 static inline int stationary(ctx* c) { c->aborted = 1; return 0; }
+/* Brent's cycle detection for the region-level loops (entry clip, region rounds,
+ * null-region skips), whose rounds are functions of (region, position) alone: a snapshot
+ * at rounds 1, 2, 4, ...; a later state equal to it repeats forever.  Finds a repeat of
+ * any period (a fixed point at the first repeat).  The kernels use the same test
+ * (vr_device.h Ctx::cycle_step); the pixel's result does not depend on when a repeat is
+ * found (colour 0, only the pixel write counted). */
+typedef struct { v3i c; v3f o; uint32_t lam, pow; } cycle;
+static inline cycle cycle_start(v3i c, v3f o) { cycle y = {c, o, 0u, 1u}; return y; }
+static inline int cycle_step(cycle* y, v3i c, v3f o) {
+    if (same_i(c, y->c) && same_v(o, y->o)) return 1;
+    if (++y->lam == y->pow) { y->c = c; y->o = o; y->pow <<= 1; y->lam = 0u; }
+    return 0;
+}
 
 /* VoxelScene::isRayInScene (Renderer.cuh:38-44) */
 static inline int in_scene(const ctx* c, v3i r) {
@@ -601,21 +614,21 @@ static uint32_t shadow_grid_original(ctx* c, ray3* ray, int32_t reg) {
 static int shadow_scene_original(ctx* c, ray3 lr, v3i cr) {
     if (!c->lit->use_shadows) return 0;
     c->in_shadow = 1;
+    cycle cyc = cycle_start(cr, lr.o);
     while (in_scene(c, cr)) {
         if (!tick(c)) return 0;
-        const v3i cr0 = cr; const v3f o0 = lr.o;
         int32_t reg = region_at(c, cr);
+        cycle cyc1 = cycle_start(cr, lr.o);
         while (reg < 0) {
             if (!tick(c)) return 0;
-            const v3i cr1 = cr; const v3f o1 = lr.o;
             if (!skip_null_region(c, &cr, &lr, 1, &reg)) return 0;
-            if (same_i(cr, cr1) && same_v(lr.o, o1)) return stationary(c);
+            if (cycle_step(&cyc1, cr, lr.o)) return stationary(c);
         }
         uint32_t col = shadow_grid_original(c, &lr, reg);
         if (c->aborted) return 0;
         if (col != EMPTY_VAL) return 1;
         advance_region(&cr, &lr);
-        if (same_i(cr, cr0) && same_v(lr.o, o0)) return stationary(c);
+        if (cycle_step(&cyc, cr, lr.o)) return stationary(c);
     }
     return 0;
 }
@@ -825,21 +838,21 @@ static uint32_t grid_longest(ctx* c, ray3* orig, v3f rwp, int32_t reg, v3i cr, i
 static int shadow_scene_longest(ctx* c, ray3 lr, v3i cr) {
     if (!c->lit->use_shadows) return 0;
     c->in_shadow = 1;
+    cycle cyc = cycle_start(cr, lr.o);
     while (in_scene(c, cr)) {
         if (!tick(c)) return 0;
-        const v3i cr0 = cr; const v3f o0 = lr.o;
         int32_t reg = region_at(c, cr);
+        cycle cyc1 = cycle_start(cr, lr.o);
         while (reg < 0) {
             if (!tick(c)) return 0;
-            const v3i cr1 = cr; const v3f o1 = lr.o;
             if (!skip_null_region(c, &cr, &lr, 0, &reg)) return 0;
-            if (same_i(cr, cr1) && same_v(lr.o, o1)) return stationary(c);
+            if (cycle_step(&cyc1, cr, lr.o)) return stationary(c);
         }
         uint32_t col = grid_longest(c, &lr, V3(0, 0, 0), reg, cr, 1);
         if (c->aborted) return 0;
         if (col != EMPTY_VAL) return 1;
         advance_region(&cr, &lr);
-        if (same_i(cr, cr0) && same_v(lr.o, o0)) return stationary(c);
+        if (cycle_step(&cyc, cr, lr.o)) return stationary(c);
     }
     return 0;
 }
@@ -852,9 +865,9 @@ static uint32_t scene_march(ctx* c, ray3 world, uint32_t scale, int algo) {
     v3i cr = {{f2i(floorf(sr.o.v[0] / (float)BLOCK)), f2i(floorf(sr.o.v[1] / (float)BLOCK)),
                f2i(floorf(sr.o.v[2] / (float)BLOCK))}};
     /* entry clip (:349-373) */
+    cycle cyc0 = cycle_start(cr, sr.o);
     while (!in_scene(c, cr)) {
         if (!tick(c)) return 0;
-        const v3i cr0 = cr; const v3f o0 = sr.o;
         int32_t hi = (int32_t)(s->D + (uint32_t)s->min_coord), lo = 0 + s->min_coord;
         int32_t nx = d.v[0] < 0.0f ? hi : lo, ny = d.v[1] < 0.0f ? hi : lo, nz = d.v[2] < 0.0f ? hi : lo;
         float tX = ((float)(nx * BLOCK) - sr.o.v[0]) / d.v[0];
@@ -869,19 +882,19 @@ static uint32_t scene_march(ctx* c, ray3 world, uint32_t scale, int algo) {
         cr.v[0] = f2i(floorf(sr.o.v[0] / (float)BLOCK));
         cr.v[1] = f2i(floorf(sr.o.v[1] / (float)BLOCK));
         cr.v[2] = f2i(floorf(sr.o.v[2] / (float)BLOCK));
-        if (same_i(cr, cr0) && same_v(sr.o, o0)) return stationary(c);
+        if (cycle_step(&cyc0, cr, sr.o)) return stationary(c);
     }
     ray3 lr = {vscale(1.0f, vsub(sr.o, V3((float)(cr.v[0] * BLOCK), (float)(cr.v[1] * BLOCK),
                                           (float)(cr.v[2] * BLOCK)))), d};
+    cycle cyc = cycle_start(cr, lr.o);
     while (in_scene(c, cr)) {
         if (!tick(c)) return 0;
-        const v3i cr0 = cr; const v3f o0 = lr.o;
         int32_t reg = region_at(c, cr);
+        cycle cyc1 = cycle_start(cr, lr.o);
         while (reg < 0) {
             if (!tick(c)) return 0;
-            const v3i cr1 = cr; const v3f o1 = lr.o;
             if (!skip_null_region(c, &cr, &lr, 0, &reg)) return 0;
-            if (same_i(cr, cr1) && same_v(lr.o, o1)) return stationary(c);
+            if (cycle_step(&cyc1, cr, lr.o)) return stationary(c);
         }
         v3f rwp = vadd(c->translation, V3((float)(cr.v[0] * BLOCK), (float)(cr.v[1] * BLOCK),
                                           (float)(cr.v[2] * BLOCK)));
@@ -890,7 +903,7 @@ static uint32_t scene_march(ctx* c, ray3 world, uint32_t scale, int algo) {
         if (c->aborted) return 0;
         if (col != EMPTY_VAL) return col;
         advance_region(&cr, &lr);
-        if (same_i(cr, cr0) && same_v(lr.o, o0)) return stationary(c);
+        if (cycle_step(&cyc, cr, lr.o)) return stationary(c);
     }
     return 0;
 }

@@ -30,6 +30,9 @@ p.add_argument("--warmup", type=int, default=20)
 p.add_argument("--frames-in-flight", type=int, default=0, help="default: tiles.pipeline_depth (bench.py's)")
 p.add_argument("--ranks", default="", help="comma-separated subset of ranks (default: all)")
 p.add_argument("--band-rows", type=int, default=8)
+p.add_argument("--layout", default="tiles", choices=["tiles", "bands"],
+               help="tiles: the 2-D deal bench.py uses for fixed tiling (round 5); bands: 8-row bands")
+p.add_argument("--tile-cols", type=int, default=16)
 p.add_argument("--latency-reps", type=int, default=30)
 a = p.parse_args()
 
@@ -43,7 +46,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import voxelraymarcher_amd as vr  # noqa: E402
-from voxelraymarcher_amd.tiles import BandGather, owned_rows  # noqa: E402
+from voxelraymarcher_amd.tiles import BandGather  # noqa: E402
 
 cfg = vr.CONFIGS[a.config]
 dev = torch.device("cuda", 0)
@@ -54,13 +57,16 @@ cam = vr.Camera.reference(W, H)
 lit = vr.setup_constant_values()
 info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
 B = a.band_rows
-words = vr.band_buffer_words(W, H, B, a.world)
+T = a.tile_cols if a.layout == "tiles" else 0
+words = vr.tile_buffer_words(W, H, B, T, a.world) if T else vr.band_buffer_words(W, H, B, a.world)
 
 
 # ONE pipeline (its streams) for every run: a second BandGather's new streams may share a
 # hardware queue (4 per process on the box) and serialise its frames (seen: the second
 # pipeline of a process ran C2's rank at 2x the time of every later one)
 pipe = BandGather(W, H, B, 0, 1, dev, depth=depth)
+pipe.bufs = [torch.empty(max(words, vr.band_buffer_words(W, H, B, 1)), dtype=torch.int32, device=dev)
+             for _ in range(depth)]
 packed = [torch.empty(words * 3, dtype=torch.uint8, device=dev) for _ in range(depth)]
 
 
@@ -68,7 +74,10 @@ def run(rank, nranks, steps):
     k = [0]
 
     def render(buf):
-        vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, B, rank, nranks, buf)
+        if T and nranks > 1:
+            vr.render_tiles(scene, cfg.algorithm, cam, lit, info, W, H, B, T, rank, nranks, buf)
+        else:
+            vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, B, rank, nranks, buf)
         if nranks > 1:                                  # the send side of bench.py's N > 1 step
             vr.pack_rgb8(buf[:words], out=packed[k[0] % depth])
         k[0] += 1
@@ -92,7 +101,7 @@ def lone(rank, nranks, schedule):
 
     def once():
         vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=B, rank=rank, nranks=nranks,
-                     stream=st, schedule=schedule)
+                     stream=st, schedule=schedule, tile_cols=T if nranks > 1 else 0)
         if nranks > 1:
             vr.pack_rgb8(buf[:words], out=packed[0])
 
@@ -117,13 +126,17 @@ for r in ([int(x) for x in a.ranks.split(",")] if a.ranks else range(a.world)):
     ms = run(r, a.world, a.steps)
     lg = lone(r, a.world, vr.Schedule.GRID)
     ll = lone(r, a.world, vr.Schedule.HEAVIEST_FIRST)
-    ranks.append({"rank": r, "rows": len(owned_rows(H, B, r, a.world)), "ms_per_frame": round(ms, 4),
+    ranks.append({"rank": r, "ms_per_frame": round(ms, 4),
                   "lone_frame_ms_grid": round(lg, 4), "lone_frame_ms_learned": round(ll, 4)})
     print(json.dumps(ranks[-1]), flush=True)
 slow = max(x["ms_per_frame"] for x in ranks)
 slow_lg = max(x["lone_frame_ms_grid"] for x in ranks)
 slow_ll = max(x["lone_frame_ms_learned"] for x in ranks)
+mean = sum(x["ms_per_frame"] for x in ranks) / len(ranks)
+mean_lg = sum(x["lone_frame_ms_grid"] for x in ranks) / len(ranks)
 print(json.dumps({"config": a.config, "width": W, "height": H, "world": a.world, "band_rows": B,
+                  "layout": a.layout, "tile_cols": T,
+                  "slowest_over_mean": round(slow / mean, 3), "slowest_over_mean_lone_grid": round(slow_lg / mean_lg, 3),
                   "frames_in_flight": depth,
                   "steps": a.steps, "one_gpu_ms_per_frame": round(single, 4),
                   "projected_ms_per_frame": slow, "projected_speedup": round(single / slow, 2),

@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import voxelraymarcher_amd as vr
-from voxelraymarcher_amd.tiles import assemble_bands, owned_rows
+from voxelraymarcher_amd.tiles import assemble_bands, assemble_tiles, owned_rows, tile_rank_buffer
 
 
 def _free_port() -> int:
@@ -164,3 +164,114 @@ def test_pipeline_policy():
     assert pipeline_hw_queues(pipeline_depth("C5")) >= pipeline_depth("C5") + 2
     # N > 1: rank 0's assembly stream and the RCCL stream join the two frame streams
     assert pipeline_hw_queues(2, 8) >= 2 + 3
+
+
+def _tile_worker(rank, world, port, W, H, B, T, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    frame = (torch.arange(W * H, dtype=torch.int64) * 2654435761 % (1 << 24)).to(torch.int32).reshape(H, W)
+    buf = tile_rank_buffer(frame, rank, world, B, T)
+    assert buf.numel() == vr.tile_buffer_words(W, H, B, T, world)
+    gathered = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gathered, dst=0)
+    if rank == 0:
+        img = assemble_tiles(torch.stack(gathered), W, H, B, T)
+        q.put(bool(torch.equal(img, frame)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H,T", [(2, 64, 45, 16), (3, 100, 37, 8), (8, 3840, 2160, 16)])
+def test_tile_gather_reassembles(world, W, H, T):
+    """The 2-D tile deal (bench.py's N > 1 layout for fixed tiling; the 8-rank case is C5's
+    3840x2160 frame): each rank's tile buffer, gathered over gloo and assembled on rank 0,
+    gives the frame back."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tile_worker, args=(r, world, port, W, H, 8, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert ok
+
+
+def _tile_pipeline_worker(rank, world, port, W, H, B, T, frames, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from voxelraymarcher_amd.tiles import BandGather
+
+    def expected(k):
+        return ((torch.arange(W * H, dtype=torch.int64) * 2654435761 + 977 * k) % (1 << 24)).to(torch.int32).reshape(H, W)
+
+    got = []
+    pipe = BandGather(W, H, B, rank, world, "cpu", depth=2, on_frame=lambda f: got.append(f.clone()), tile_cols=T)
+    assert pipe.T == T
+    k_box = [0]
+
+    def render(buf):
+        buf.copy_(tile_rank_buffer(expected(k_box[0]), rank, world, B, T))
+
+    for k in range(frames):
+        k_box[0] = k
+        pipe.step(render)
+    pipe.drain()
+    if rank == 0:
+        q.put([bool(torch.equal(g, expected(k))) for k, g in enumerate(got)])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tile_gather_pipeline_overlapped(world):
+    """BandGather with the 2-D tile deal: frames intact and in order, two in flight."""
+    W, H, B, T, frames = 72, 61, 8, 16, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tile_pipeline_worker, args=(r, world, port, W, H, B, T, frames, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [True] * frames
+
+
+def _exchange_worker(rank, world, port, q):
+    """One rank with the exchange forced (bench.py --exchange): the gather/assembly path runs."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from voxelraymarcher_amd.tiles import BandGather
+    W, H, B = 40, 21, 8
+    ref = torch.arange(W * H, dtype=torch.int32).reshape(H, W)
+    got = []
+    for T in (0, 16):
+        pipe = BandGather(W, H, B, 0, 1, "cpu", on_frame=lambda f: got.append(f.clone()), tile_cols=T,
+                          exchange=True)
+        assert pipe.x and pipe.T == T
+
+        def render(buf, T=T):
+            if T:
+                buf.copy_(tile_rank_buffer(ref, 0, 1, B, T))
+            else:
+                buf.view(-1, W)[:H] = ref
+        pipe.step(render)
+        pipe.drain()
+    q.put(len(got) == 2 and all(torch.equal(g, ref) for g in got))
+    dist.destroy_process_group()
+
+
+def test_forced_exchange_single_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_exchange_worker, args=(0, 1, _free_port(), q))
+    p.start()
+    ok = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and ok

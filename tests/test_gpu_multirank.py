@@ -45,15 +45,46 @@ def _oracle_rgb8(cfg_name: str, W: int, H: int) -> np.ndarray:
     return np.stack([(w >> 16) & 0xFF, (w >> 8) & 0xFF, w & 0xFF], axis=-1).astype(np.uint8)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_bench_frame_path_ranks_share_one_gpu(world, tmp_path):
+def _run_bench(world, extra, tmp_path, W=480, H=270):
+    dump = tmp_path / "frame.npy"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--steps", "4", "--warmup", "2", "--config", "C2", "--tiling", "fixed",
+           "--resolution", f"{W}x{H}", "--no-cpu-baseline", "--dump-frame", str(dump)] + extra
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, f"bench.py over {world} ranks failed:\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0]), np.load(dump)
+
+
+def test_rccl_gather_one_rank(tmp_path):
+    """The RCCL branch of the N > 1 path on a one-GPU box (RCCL refuses two ranks on one
+    device): bench.py --exchange --backend nccl starts a one-rank nccl process group
+    (init_process_group("nccl", device_id=...), tiles.init_frame_group), renders the 2-D tile
+    layout, packs RGB8, gathers it with dist.gather on the slot stream over RCCL, and rank 0
+    assembles it with the device kernel (vr_assemble_tiles) on its side stream; the frame
+    equals the oracle's, byte for byte."""
+    W, H = 480, 270
+    line, got = _run_bench(1, ["--exchange", "--backend", "nccl"], tmp_path, W, H)
+    assert line["n_gpus"] == 1 and "RCCL gather" in line["config"]["parallelism"]
+    assert line["config"]["layout"] == "tiles" and line["dispatch_phases"]["latency"] == 5
+    want = _oracle_rgb8("C2", W, H)
+    assert got.shape == (H, W, 3) and got.dtype == np.uint8
+    bad = int(np.count_nonzero(np.any(got != want, axis=-1)))
+    assert bad == 0, f"{bad} of {W * H} pixels of the RCCL-gathered RGB8 frame differ from the oracle"
+
+
+@pytest.mark.parametrize("world,layout", [(2, "tiles"), (3, "tiles"), (2, "bands")])
+def test_bench_frame_path_ranks_share_one_gpu(world, layout, tmp_path):
     W, H = 480, 270
     dump = tmp_path / "frame.npy"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
            "--gpus", str(world), "--steps", "4", "--warmup", "2", "--config", "C2", "--tiling", "fixed",
            "--resolution", f"{W}x{H}", "--backend", "gloo", "--same-device", "--no-cpu-baseline",
-           "--dump-frame", str(dump)]
+           "--layout", layout, "--dump-frame", str(dump)]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, f"bench.py over {world} ranks failed:\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
@@ -63,7 +94,7 @@ def test_bench_frame_path_ranks_share_one_gpu(world, tmp_path):
     assert line["n_gpus"] == world and line["scaling"] == "strong"
     assert (line["config"]["width"], line["config"]["height"]) == (W, H)
     assert line["frame_latency_ms"] > 0 and line["ms_per_step"] > 0 and line["value"] > 0
-    assert "gloo" in line["config"]["parallelism"]
+    assert "gloo" in line["config"]["parallelism"] and line["config"]["layout"] == layout
     assert line["dispatch_phases"]["latency"] == 5
     # the frame's algorithmic bytes are the sum over the ranks' bands (all-reduced)
     assert line["roofline"]["algorithmic_bytes_per_frame"] > line["roofline"]["algorithmic_bytes_per_launch"]

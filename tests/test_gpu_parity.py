@@ -169,27 +169,41 @@ def test_c5_crawl_pixels_fixture(c5):
                 assert int(got[(p["y"] - 696) * cfg.width + p["x"]]) == p["colour"], p
 
 
-def test_c5_eight_rank_emulation(c5):
-    """C5 as BASELINE defines it -- the fixed 3840x2160 frame cut into 8-row bands dealt
-    round-robin to 8 ranks -- emulated on one GPU: each rank's vr_render_bands buffer,
-    assembled, equals the oracle's frame."""
+@pytest.mark.parametrize("layout", ["tiles", "bands"])
+def test_c5_eight_rank_emulation(c5, layout):
+    """C5 as BASELINE defines it -- the fixed 3840x2160 frame over 8 ranks -- emulated on
+    one GPU: each rank's buffer, assembled, equals the oracle's frame.  layout "tiles":
+    the 2-D deal bench.py uses (8x16 blocks, block j of band b -> rank (j + 3b) % 8;
+    vr_render_tiles + the device assembly kernel), both algorithms; "bands": 8-row bands
+    dealt round-robin (vr_render_bands)."""
     import torch
 
     from voxelraymarcher_amd.tiles import assemble_bands
     cfg, xyz, rgb, g, o, frames = c5
-    W, H, R, B = cfg.width, cfg.height, 8, 8
+    W, H, R, B, T = cfg.width, cfg.height, 8, 8, 16
     cam, lit = vr.Camera.reference(W, H), vr.setup_constant_values()
     info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
-    words = vr.band_buffer_words(W, H, B, R)
-    parts = []
-    for r in range(R):
-        buf = torch.full((words,), -7, dtype=torch.int32, device="cuda")
-        vr.render_bands(g, vr.RayMarchAlgorithm.ORIGINAL, cam, lit, info, W, H, B, r, R, buf)
-        parts.append(buf)
-    torch.cuda.synchronize()
-    img = assemble_bands(torch.stack(parts), W, H, B).cpu().numpy().view(np.uint32).reshape(-1)
-    want = frames[vr.RayMarchAlgorithm.ORIGINAL][0]
-    assert np.array_equal(img, want), diff_report(img, want, W)
+    for algo in (ALGOS if layout == "tiles" else [vr.RayMarchAlgorithm.ORIGINAL]):
+        if layout == "tiles":
+            words = vr.tile_buffer_words(W, H, B, T, R)
+            parts = torch.full((R, words), -7, dtype=torch.int32, device="cuda")
+            for r in range(R):
+                vr.render_tiles(g, algo, cam, lit, info, W, H, B, T, r, R, parts[r])
+            frame = torch.empty((H, W), dtype=torch.int32, device="cuda")
+            vr.assemble_tiles_device(parts, frame, 4, W, H, B, T, R)
+            torch.cuda.synchronize()
+            img = frame.cpu().numpy().view(np.uint32).reshape(-1)
+        else:
+            words = vr.band_buffer_words(W, H, B, R)
+            parts = []
+            for r in range(R):
+                buf = torch.full((words,), -7, dtype=torch.int32, device="cuda")
+                vr.render_bands(g, algo, cam, lit, info, W, H, B, r, R, buf)
+                parts.append(buf)
+            torch.cuda.synchronize()
+            img = assemble_bands(torch.stack(parts), W, H, B).cpu().numpy().view(np.uint32).reshape(-1)
+        want = frames[algo][0]
+        assert np.array_equal(img, want), f"{layout} {algo.name}: " + diff_report(img, want, W)
 
 
 def test_alias_rays():

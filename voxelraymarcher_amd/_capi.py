@@ -50,13 +50,15 @@ class VrSynthParams(ctypes.Structure):
 
 VR_KERNEL_AUTO, VR_KERNEL_TILE, VR_KERNEL_TILE_REWALK = 0, 1, 3
 VR_SCHEDULE_AUTO, VR_SCHEDULE_GRID, VR_SCHEDULE_HEAVIEST_FIRST = 0, 1, 2
+VR_OCCUPANCY_AUTO, VR_OCCUPANCY_LONE, VR_OCCUPANCY_IN_FLIGHT = 0, 1, 2
 
 
 class VrRenderOpts(ctypes.Structure):
     """vr_render_opts (versioned by its leading struct_size; VR_RENDER_OPTS_MIN_SIZE = 48)."""
     _fields_ = [("struct_size", c_uint32), ("kernel", c_uint32), ("row_begin", c_uint32), ("row_end", c_uint32),
                 ("band_rows", c_uint32), ("rank", c_uint32), ("nranks", c_uint32), ("defer_cap", c_uint32),
-                ("bytes_dev", c_void_p), ("schedule", c_uint32), ("reserved", c_uint32), ("stats_dev", c_void_p)]
+                ("bytes_dev", c_void_p), ("schedule", c_uint32), ("reserved", c_uint32), ("stats_dev", c_void_p),
+                ("occupancy", c_uint32), ("tile_cols", c_uint32), ("deal_stride", c_uint32), ("reserved2", c_uint32)]
 
 
 VR_RENDER_OPTS_MIN_SIZE = 48
@@ -87,6 +89,13 @@ SIGNATURES = {
     "vr_render_bands": (c_int, [c_void_p, c_int, POINTER(VrCamera), POINTER(VrLighting), POINTER(c_float),
                                 c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p, c_void_p]),
     "vr_band_buffer_words": (c_uint64, [c_uint32, c_uint32, c_uint32, c_uint32]),
+    "vr_render_tiles": (c_int, [c_void_p, c_int, POINTER(VrCamera), POINTER(VrLighting), POINTER(c_float),
+                                c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p,
+                                c_void_p]),
+    "vr_tile_buffer_words": (c_uint64, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint32]),
+    "vr_deal_stride_default": (c_uint32, [c_uint32]),
+    "vr_assemble_tiles": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32,
+                                  c_uint32, c_void_p]),
     "vr_render_ex": (c_int, [c_void_p, c_int, POINTER(VrCamera), POINTER(VrLighting), POINTER(c_float), c_uint32,
                              c_uint32, c_uint32, POINTER(VrRenderOpts), c_void_p, c_void_p]),
     "vr_render_opts_init": (c_int, [POINTER(VrRenderOpts)]),
@@ -132,6 +141,9 @@ def f3(v) -> ctypes.Array:
     return (c_float * 3)(*[float(x) for x in v])
 
 
-__all__ = ["lib", "check", "VrCamera", "VrLighting", "VrRenderOpts", "VR_RENDER_OPTS_MIN_SIZE","VR_KERNEL_AUTO", "VR_KERNEL_TILE", "VR_KERNEL_TILE_REWALK", "VR_SCHEDULE_AUTO", "VR_SCHEDULE_GRID", "VR_SCHEDULE_HEAVIEST_FIRST", "VrSceneInfo", "VrSynthParams", "VrError", "SIGNATURES",
+__all__ = ["lib", "check", "VrCamera", "VrLighting", "VrRenderOpts", "VR_RENDER_OPTS_MIN_SIZE", "VR_KERNEL_AUTO",
+           "VR_KERNEL_TILE", "VR_KERNEL_TILE_REWALK", "VR_SCHEDULE_AUTO", "VR_SCHEDULE_GRID",
+           "VR_SCHEDULE_HEAVIEST_FIRST", "VR_OCCUPANCY_AUTO", "VR_OCCUPANCY_LONE", "VR_OCCUPANCY_IN_FLIGHT",
+           "VrSceneInfo", "VrSynthParams", "VrError", "SIGNATURES",
            "VR_STORE_VCS", "VR_STORE_HASHTABLE", "VR_ALGO_LONGESTAXIS", "VR_ALGO_ORIGINAL", "f3", "LIB_PATH",
            "c_uint8"]

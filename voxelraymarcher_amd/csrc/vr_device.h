@@ -187,9 +187,8 @@ struct Ctx {
     uint32_t iters = 0;
     bool aborted = false;
     uint32_t bytes = 0;
-    // crawl pass (BUDGET == kCrawlBudget) with the scene cached in LDS: the region table
-    const uint32_t* lrt = nullptr;
     uint32_t ff = 0;     // (COUNT) crawl iterations credited in closed form (crawl_run)
+    uint32_t nl = 0;     // (COUNT) crawl-pass skip steps answered from the LDS cluster bits (counted, not loaded)
 #ifdef VR_CRAWL_PROF
     uint32_t d_runs = 0, d_trips = 0;   // (diagnostic builds) crawl_run calls that applied steps, their loop trips
 #endif
@@ -226,9 +225,6 @@ struct Ctx {
         uint32_t mc = (uint32_t)s.min_coord;
         uint32_t ux = (uint32_t)r.x - mc, uy = (uint32_t)r.y - mc, uz = (uint32_t)r.z - mc;
         count(4);
-        if constexpr (BUDGET == kCrawlBudget) {
-            if (lrt) return lrt[ux + uy * s.D + uz * s.D * s.D];
-        }
         return s.region_slot[ux + uy * s.D + uz * s.D * s.D];
     }
 
@@ -237,9 +233,6 @@ struct Ctx {
     __device__ __forceinline__ uint32_t region_at_nocount(i3 r) const {
         uint32_t mc = (uint32_t)s.min_coord;
         uint32_t ux = (uint32_t)r.x - mc, uy = (uint32_t)r.y - mc, uz = (uint32_t)r.z - mc;
-        if constexpr (BUDGET == kCrawlBudget) {
-            if (lrt) return lrt[ux + uy * s.D + uz * s.D * s.D];
-        }
         return s.region_slot[ux + uy * s.D + uz * s.D * s.D];
     }
 
@@ -453,6 +446,29 @@ struct Ctx {
     __device__ __forceinline__ static bool same_pos(i3 ca, f3 a, i3 cb, f3 b) {
         return ca.x == cb.x && ca.y == cb.y && ca.z == cb.z && same_f(a.x, b.x) && same_f(a.y, b.y) &&
                same_f(a.z, b.z);
+    }
+    // Brent's cycle detection over a loop's state (cr, o) (crawl pass): a snapshot is taken at
+    // rounds 1, 2, 4, 8, ... and every later state is compared with it, so a loop whose state
+    // repeats -- after any prefix, with any period -- is found within about twice (prefix +
+    // period) rounds.  Every round of the reference's region, null-region and entry-clip loops
+    // is a function of this state alone, so a repeat means the reference never returns; the
+    // pixel is then declared non-terminating.  (Round 4 compared each round with
+    // the one before only, which finds period-1 repeats: fixed points.)
+    struct Cycle {
+        i3 c;
+        f3 o;
+        uint32_t lam, pow;
+    };
+    __device__ __forceinline__ static Cycle cycle_start(i3 c, f3 o) { return Cycle{c, o, 0u, 1u}; }
+    __device__ __forceinline__ static bool cycle_step(Cycle& y, i3 c, f3 o) {
+        if (same_pos(c, o, y.c, y.o)) return true;
+        if (++y.lam == y.pow) {
+            y.c = c;
+            y.o = o;
+            y.pow <<= 1;
+            y.lam = 0u;
+        }
+        return false;
     }
     __device__ __forceinline__ static bool grid_in_region(int32_t a, int32_t b, int32_t c) {   // :436-439
         return (uint32_t)a < 64u && (uint32_t)b < 64u && (uint32_t)c < 64u;

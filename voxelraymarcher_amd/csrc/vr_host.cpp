@@ -498,6 +498,7 @@ int make_view(const vr_scene* s, const vr_camera* cam, const vr_lighting* lit, c
     v.use_shadows = lit->use_shadows ? 1 : 0;
     v.W = width;
     v.H = height;
+    v.LW = width;
     return VR_OK;
 }
 
@@ -638,18 +639,6 @@ uint32_t crawl_rpw_override() {
     }();
     return r;
 }
-// VR_CRAWL_SCENE_LDS=1 (A/B runs): the crawl pass caches the scene's region table and
-// cluster bits in each workgroup's LDS when they fit.  Off by default: measured no faster
-// than the per-record bit slots for a lone C5 frame (0.806 vs 0.801 ms) and slower with
-// frames in flight (0.677 vs 0.636 ms per frame; one 108-KB workgroup per CU),
-// profiles/r04/crawl/scene_lds_ab.txt.
-bool crawl_scene_lds_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("VR_CRAWL_SCENE_LDS");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
 // VR_INFLIGHT_WAVES=0 (A/B runs): frames in flight keep the lone-frame occupancy.
 bool in_flight_occupancy() {
     static const bool on = [] {
@@ -666,14 +655,26 @@ bool order_enabled() {
     return on;
 }
 
-int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, vr::KView& v, void* stream) {
+int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, uint32_t occupancy, vr::KView& v,
+           void* stream) {
     if (algo != VR_ALGO_ORIGINAL && algo != VR_ALGO_LONGESTAXIS) return fail(VR_E_INVALID, "unknown algorithm");
     if (kernel != VR_KERNEL_AUTO && kernel != VR_KERNEL_TILE && kernel != VR_KERNEL_TILE_REWALK)
         return fail(VR_E_INVALID, "unknown kernel (2, the persistent kernel, was retired)");
-    if (v.local_rows == 0 || v.W == 0) return VR_OK;
+    if (occupancy > VR_OCCUPANCY_IN_FLIGHT) return fail(VR_E_INVALID, "unknown occupancy");
+    if (v.local_rows == 0 || v.LW == 0) return VR_OK;
     DeviceGuard dg(s->device);
     const bool count = v.bytes != nullptr;
     const hipStream_t st = (hipStream_t)stream;
+    // A launch is not capturable into a graph: the slot ring's event wait/record and the
+    // work order's host-side bookkeeping would be baked into it and not replay (no test
+    // captures one), so capture is refused before anything is enqueued.
+    {
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        const hipError_t e = hipStreamIsCapturing(st, &cap);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamIsCapturing");
+        if (cap != hipStreamCaptureStatusNone)
+            return fail(VR_E_INVALID, "vr_render* cannot be captured into a HIP graph (stream is capturing)");
+    }
     v.crawl_rewalk = kernel == VR_KERNEL_TILE_REWALK ? 1u : 0u;
     // the deferral list of the crawl pass (cluster-skip crawls, walks over the tile budget)
     SlotLease lease;
@@ -695,12 +696,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     bool remake = false;
     // (the lock orders launches: "previous" is well defined)
     const bool alone = !D.any || D.last_stream == st || hipEventQuery(D.ev[D.last_idx]) == hipSuccess;
-    bool heavy = schedule == VR_SCHEDULE_HEAVIEST_FIRST || (schedule == VR_SCHEDULE_AUTO && alone);
-    // A launch captured into a graph renders in grid order: the order's host-side
-    // bookkeeping (age, remake) would not replay with the graph, and its buffers are
-    // stream-ordered allocations.
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) heavy = false;
+    const bool heavy = schedule == VR_SCHEDULE_HEAVIEST_FIRST || (schedule == VR_SCHEDULE_AUTO && alone);
     // crawl records per wave: a lone frame ends with the crawl pass's longest chain (2 per
     // wave since round 4's shorter chains: C5 alone 0.767 -> 0.759 ms vs 4,
     // profiles/r04/crawl/scene_lds_ab.txt, rpw_multi_cluster.txt); with frames in flight the
@@ -736,14 +732,15 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         remake = !match || ++O.age >= order_refresh();
         v.cost = remake ? O.cost : nullptr;
     }
-    // crawl pass: the scene cached in each workgroup's LDS when it fits and records are
-    // expected (a hint from an earlier launch: any shape renders the same pixels)
+    // crawl pass grid from the records an earlier launch deferred (a hint: any grid renders
+    // the same pixels)
     const vr::KScene ks = kscene(s);
-    v.crawl_scene_lds = (s->store == VR_STORE_VCS && expect > 0 && crawl_scene_lds_enabled() && vr::crawl_lds_fits(ks))
-                            ? 1u : 0u;
-    const uint32_t cwgs = v.crawl_scene_lds ? vr::crawl_grid_scene_lds(expect, v.crawl_rpw)
-                                            : vr::crawl_grid(expect, v.crawl_rpw);
-    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs, !alone && in_flight_occupancy());
+    const uint32_t cwgs = vr::crawl_grid(expect, v.crawl_rpw);
+    // the tile pass's occupancy variant (vr_occupancy): AUTO = the in-flight one while another
+    // stream's launch is running
+    const bool hi = occupancy == VR_OCCUPANCY_IN_FLIGHT ||
+                    (occupancy == VR_OCCUPANCY_AUTO && !alone && in_flight_occupancy());
+    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs, hi);
     if (e == hipSuccess && remake) {
         // (on a side stream instead -- one more stream than the box's 4 hardware queues
         // serialised the two render streams: C2 0.1124 -> 0.1277 ms per frame in flight,
@@ -1077,21 +1074,38 @@ int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr
     const uint32_t row_end = o.row_end == 0xFFFFFFFFu ? height : o.row_end;
     if (o.row_begin > row_end || row_end > height) return fail(VR_E_INVALID, "bad row range");
     if (!o.nranks || o.rank >= o.nranks) return fail(VR_E_INVALID, "bad band partition");
+    if (o.reserved2 != 0u) return fail(VR_E_INVALID, "vr_render_opts.reserved2 must be 0");
     const uint32_t rows = row_end - o.row_begin;
     const uint32_t band = o.band_rows ? o.band_rows : std::max(1u, rows);
     v.row0 = o.row_begin;
     v.row_limit = row_end;
     v.band_rows = band;
     v.band_minv = band == 1u ? 0xFFFFFFFFu : (uint32_t)((1ull << 32) / band);
-    v.rank = o.rank;
-    v.nranks = o.nranks;
-    v.local_rows = (uint32_t)(vr_band_buffer_words(width, rows, band, o.nranks) / width);
+    if (o.tile_cols == 0u) {
+        v.rank = o.rank;
+        v.nranks = o.nranks;
+        v.local_rows = (uint32_t)(vr_band_buffer_words(width, rows, band, o.nranks) / width);
+    } else {
+        // 2-D tile deal: every band is this rank's; its columns are dealt (KView)
+        if (o.tile_cols > width) return fail(VR_E_INVALID, "tile_cols larger than the frame width");
+        v.rank = 0;
+        v.nranks = 1;
+        v.local_rows = (uint32_t)(((uint64_t)rows + band - 1) / band * band);
+        const uint32_t nblk = (width + o.tile_cols - 1) / o.tile_cols;
+        v.LW = (nblk + o.nranks - 1) / o.nranks * o.tile_cols;
+        v.tile_cols = o.tile_cols;
+        v.tile_minv = o.tile_cols == 1u ? 0xFFFFFFFFu : (uint32_t)((1ull << 32) / o.tile_cols);
+        v.col_R = o.nranks;
+        v.col_rank = o.rank;
+        v.col_stride = (o.deal_stride ? o.deal_stride : vr_deal_stride_default(o.nranks)) % o.nranks;
+        if (v.local_rows > 65535u || v.LW > 65535u) return fail(VR_E_INVALID, "tile buffer too large");
+    }
     v.out = out_dev;
     v.bytes = (unsigned long long*)o.bytes_dev;
     v.stats = o.bytes_dev ? (unsigned long long*)o.stats_dev : nullptr;
     v.defer_cap = o.defer_cap;
     if (o.schedule > VR_SCHEDULE_HEAVIEST_FIRST) return fail(VR_E_INVALID, "unknown schedule");
-    return launch(s, algo, o.kernel, o.schedule, v, stream);
+    return launch(s, algo, o.kernel, o.schedule, o.occupancy, v, stream);
 }
 
 int vr_render_opts_init(vr_render_opts* opts) {
@@ -1130,6 +1144,50 @@ uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_row
     uint64_t nb = (height + (uint64_t)band_rows - 1) / band_rows;
     uint64_t per = (nb + nranks - 1) / nranks;
     return per * band_rows * (uint64_t)width;
+}
+
+uint32_t vr_deal_stride_default(uint32_t nranks) {
+    return (nranks % 3u == 0u) ? 1u : 3u;
+}
+
+uint64_t vr_tile_buffer_words(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t tile_cols, uint32_t nranks) {
+    if (!nranks || !tile_cols || !width || !height) return 0;
+    const uint64_t band = band_rows ? band_rows : height;
+    const uint64_t rows = (height + band - 1) / band * band;
+    const uint64_t nblk = ((uint64_t)width + tile_cols - 1) / tile_cols;
+    return rows * ((nblk + nranks - 1) / nranks * tile_cols);
+}
+
+int vr_render_tiles(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,
+                    const float translation[3], uint32_t scale, uint32_t width, uint32_t height, uint32_t band_rows,
+                    uint32_t tile_cols, uint32_t rank, uint32_t nranks, uint32_t* out_dev, void* stream) {
+    if (!band_rows || !tile_cols) return fail(VR_E_INVALID, "band_rows and tile_cols must be > 0");
+    vr_render_opts o = opts_rows(0, height);
+    o.band_rows = band_rows;
+    o.tile_cols = tile_cols;
+    o.rank = rank;
+    o.nranks = nranks;
+    return vr_render_ex(s, algo, cam, lit, translation, scale, width, height, &o, out_dev, stream);
+}
+
+int vr_assemble_tiles(const void* parts_dev, void* frame_dev, uint32_t elem_bytes, uint32_t width, uint32_t height,
+                      uint32_t band_rows, uint32_t tile_cols, uint32_t nranks, uint32_t deal_stride, void* stream) {
+    if (!parts_dev || !frame_dev) return fail(VR_E_INVALID, "NULL device buffer");
+    if (elem_bytes < 1u || elem_bytes > 4u) return fail(VR_E_INVALID, "elem_bytes must be 1..4");
+    if (!width || !height || !band_rows || !tile_cols || !nranks || tile_cols > width)
+        return fail(VR_E_INVALID, "bad tile layout");
+    vr::TileLayout t{};
+    t.W = width;
+    t.H = height;
+    t.band_rows = band_rows;
+    t.tile_cols = tile_cols;
+    t.R = nranks;
+    t.stride = (deal_stride ? deal_stride : vr_deal_stride_default(nranks)) % nranks;
+    t.LW = (uint32_t)(vr_tile_buffer_words(width, band_rows, band_rows, tile_cols, nranks) / band_rows);
+    t.rank_words = vr_tile_buffer_words(width, height, band_rows, tile_cols, nranks);
+    hipError_t e = vr::launch_assemble_tiles(parts_dev, frame_dev, elem_bytes, t, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "assemble_tiles launch");
+    return VR_OK;
 }
 
 int vr_render_bands(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr_lighting* lit,

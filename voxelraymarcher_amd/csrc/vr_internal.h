@@ -70,7 +70,12 @@ struct KScene {
 // Per-launch view: camera, lighting, scene transform and the row mapping.
 // Local row l of the output maps to frame row
 //   y = row0 + ((l / band_rows) * nranks + rank) * band_rows + (l % band_rows);
-// rows with y >= row_limit (<= H) are written as 0.
+// rows with y >= row_limit (<= H) are written as 0.  The output's rows are LW words
+// (= W, or the 2-D tile deal's local width).  2-D tile deal (tile_cols > 0; the row
+// deal then has nranks = 1, rank = 0): local column x of band b = l / band_rows maps to
+// frame column
+//   X = ((x / tile_cols) * col_R + (col_rank - col_stride * b) mod col_R) * tile_cols + x % tile_cols;
+// columns with X >= W are written as 0.
 struct KView {
     float llc[3], hor[3], ver[3], org[3];
     float L[3], LC[3], LP[3];
@@ -92,6 +97,10 @@ struct KView {
     uint32_t W, H;
     uint32_t row0, band_rows, rank, nranks, local_rows, row_limit;
     uint32_t band_minv;       // floor(2^32 / band_rows) (2^32 - 1 for 1): l / band_rows by a multiply-high
+    uint32_t LW;              // output row stride in words (local columns)
+    uint32_t tile_cols;       // 0: whole rows (no column deal)
+    uint32_t tile_minv;       // floor(2^32 / tile_cols) (2^32 - 1 for 1)
+    uint32_t col_R, col_rank, col_stride;   // 2-D deal: ranks, this rank, stride (< col_R)
     uint32_t* out;
     unsigned long long* bytes;
     // (COUNT launches, optional) [0] crawl iterations the crawl pass fast-forwarded in
@@ -100,10 +109,7 @@ struct KView {
     uint32_t* defer;         // crawl deferral slot: [count, done, overflow, 0, records (kDeferRecWords each)...]
     uint32_t defer_cap;
     uint32_t crawl_rewalk;    // 1: deferred crawls are walked from the pixel's start (VR_KERNEL_TILE_REWALK)
-    uint32_t crawl_rpw;       // crawl records per wave (0 = 4): 4 for a lone frame, 8 with frames in flight
-    // crawl pass: 1 = each workgroup caches the scene's region table and cluster-existence
-    // bits in LDS (crawl_lds_bytes, vr_march.hip crawl_kernel); 0 = per-record bit slots
-    uint32_t crawl_scene_lds;
+    uint32_t crawl_rpw;       // crawl records per wave (0 = 4): 2 for a lone frame, 8 with frames in flight
     uint32_t* defer_stat;     // host-mapped word: the crawl pass writes its record count there (grid sizing)
     // Tile-pass work order ("Heaviest tiles first"): workgroup i of the grid
     // renders tile order[i] = (tile row << 16 | tile column) -- a permutation of the grid
@@ -140,16 +146,19 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
                         hipStream_t stream, uint32_t crawl_wgs, bool in_flight);
 // Crawl-pass grid for a launch that expects about `records` deferred pixels.
 uint32_t crawl_grid(uint32_t records, uint32_t rpw);
-// The crawl pass's shape (vr_march.hip): threads per workgroup and dynamic LDS bytes for the
-// scene-cached mode (v.crawl_scene_lds) or the per-record mode; crawl_lds_fits: the scene's
-// region table and cluster bits fit one workgroup's LDS.
-uint32_t crawl_threads(bool scene_lds);
-uint32_t crawl_lds_bytes(const KScene& s, bool scene_lds);
-bool crawl_lds_fits(const KScene& s);
-uint32_t crawl_grid_scene_lds(uint32_t records, uint32_t rpw);
 // vcs_cbits of a VCS scene from its mask records (one thread per 32 cluster slots).
 hipError_t launch_cluster_bits(const uint2* vcs_mask, uint32_t n_regions, uint32_t* cbits, hipStream_t stream);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);
+// The 2-D tile deal's layout (vr_render_opts.tile_cols) for rank 0's reassembly: the frame
+// W x H, bands of band_rows rows, column blocks of tile_cols, R ranks dealt with `stride`;
+// LW = local row width (words), rank_words = one rank's buffer (pixels).
+struct TileLayout {
+    uint32_t W, H, band_rows, tile_cols, R, stride, LW;
+    uint64_t rank_words;
+};
+// frame[y][x] <- parts[rank][local pixel] for every frame pixel, elem_bytes (1..4) per pixel.
+hipError_t launch_assemble_tiles(const void* parts, void* frame, uint32_t elem_bytes, const TileLayout& t,
+                                 hipStream_t stream);
 // The tile pass's grid for a view (columns, rows of workgroups) and its waves per workgroup.
 void march_grid(const KView& v, uint32_t& columns, uint32_t& rows);
 constexpr uint32_t kWavesPerTileGroup = 2;

@@ -313,8 +313,6 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
     // clusters: a skip step reads one LDS word instead.
     uint32_t* lbm = nullptr;
     uint32_t bm_reg = kNone;
-    // (crawl pass, scene cached in LDS) every region's cluster-existence bits, 16 words each
-    const uint32_t* lbits = nullptr;
 
     // rayMarchVoxelGrid (Renderer.cuh:260-336) and, SHADOW, shadowRayMarchVoxelGrid (:100-172).
     // The cluster-skip step (:290-306) and the voxel step (:318-331) share one
@@ -394,9 +392,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             // the scene's, or this lane's slot, refilled when the walk enters another region
             const uint32_t* bits = nullptr;
             if constexpr (CRAWL) {
-                if (lbits) {
-                    bits = lbits + reg * 16u;
-                } else if (lbm) {
+                if (lbm) {
                     if (reg != bm_reg) {
                         const uint4* src = reinterpret_cast<const uint4*>(s.vcs_cbits + (size_t)reg * 16u);
                         const uint4 b0 = src[0], b1 = src[1], b2 = src[2], b3 = src[3];
@@ -489,6 +485,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                             if constexpr (CRAWL) {
                                 // (crawl pass) cluster slot wi >> 4 absent per the LDS bits: no load
                                 const bool pres = !bits || ((bits[wi >> 9] >> ((wi >> 4) & 31u)) & 1u);
+                                if (COUNT && !pres) ++this->nl;   // counted above, never loaded
                                 blk = Blk{0u, kNone};
                                 if (pres)
                                     blk = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) +
@@ -1313,11 +1310,10 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
         const Rcp rc[3] = {rcp_setup(d.x), rcp_setup(d.y), rcp_setup(d.z)};
         i3 cr{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
         VR_DIAG_COUNT(14);                            // primary() calls
+        auto cyc = this->cycle_start(cr, so);     // (kExact only: dead code in the tile pass)
         while (!in_scene(cr)) {                   // entry clip (:349-373)
             if (!tick()) return false;
             VR_DIAG_COUNT(15);
-            const i3 cr0 = cr;
-            const f3 so0 = so;
             int32_t hi = (int32_t)(s.D + (uint32_t)s.min_coord), lo = s.min_coord;
             int32_t nx = d.x < 0.0f ? hi : lo, ny = d.y < 0.0f ? hi : lo, nz = d.z < 0.0f ? hi : lo;
             const float ax = (float)(nx * kBlock) - so.x, ay = (float)(ny * kBlock) - so.y,
@@ -1339,7 +1335,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             if (tMin == kInf) return false;
             so = add(so, scl(tMin + kEps, d));
             cr = i3{f2i(floorf(so.x / 64.0f)), f2i(floorf(so.y / 64.0f)), f2i(floorf(so.z / 64.0f))};
-            if (kExact && this->same_pos(cr, so, cr0, so0)) { aborted = true; return false; }   // never ends
+            if (kExact && this->cycle_step(cyc, cr, so)) { aborted = true; return false; }   // never ends
         }
         f3 o = sub(so, mk((float)(cr.x * kBlock), (float)(cr.y * kBlock), (float)(cr.z * kBlock)));
         return primary_regions<ALGO>(o, d, cr, h, nullptr, rc);
@@ -1355,21 +1351,19 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             if (hit) return true;
             advance_region(cr, o);
         }
+        auto cyc = this->cycle_start(cr, o);
         while (in_scene(cr)) {
             if (!tick()) return false;
             VR_DIAG_COUNT(10);                         // primary region rounds
-            const i3 cr0 = cr;
-            const f3 o0 = o;
             uint32_t reg = region_at(cr);
+            auto cyc1 = this->cycle_start(cr, o);
             while (reg == kNone) {
                 if (!tick()) return false;
                 VR_DIAG_COUNT(11);                     // null-region skips
-                const i3 cr1 = cr;
-                const f3 o1 = o;
                 if (!this->template skip_null<false>(cr, o, d, reg)) return false;
-                // kExact: a round that changes nothing repeats forever (the reference never
+                // kExact: a loop whose state repeats never ends (the reference never
                 // returns); the VCS tile pass hands such pixels over through its budget
-                if (kExact && this->same_pos(cr, o, cr1, o1)) { aborted = true; return false; }
+                if (kExact && this->cycle_step(cyc1, cr, o)) { aborted = true; return false; }
             }
             bool hit = ALGO == ALGO_ORIGINAL ? grid_original<false>(o, d, reg, cr, h, nullptr, rc)
                                              : (STORE == STORE_VCS ? grid_longest_vcs<false>(o, d, reg, cr, h)
@@ -1377,7 +1371,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
-            if (kExact && this->same_pos(cr, o, cr0, o0)) { aborted = true; return false; }
+            if (kExact && this->cycle_step(cyc, cr, o)) { aborted = true; return false; }
         }
         return false;
     }
@@ -1397,19 +1391,17 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             if (hit) return true;
             advance_region(cr, o);
         }
+        auto cyc = this->cycle_start(cr, o);
         while (in_scene(cr)) {
             if (!tick()) return false;
             VR_DIAG_COUNT(12);                         // shadow region rounds
-            const i3 cr0 = cr;
-            const f3 o0 = o;
             uint32_t reg = region_at(cr);
+            auto cyc1 = this->cycle_start(cr, o);
             while (reg == kNone) {
                 if (!tick()) return false;
                 VR_DIAG_COUNT(13);
-                const i3 cr1 = cr;
-                const f3 o1 = o;
                 if (!this->template skip_null<!LONGEST>(cr, o, d, reg)) return false;
-                if (kExact && this->same_pos(cr, o, cr1, o1)) { aborted = true; return false; }   // (as above)
+                if (kExact && this->cycle_step(cyc1, cr, o)) { aborted = true; return false; }   // (as above)
             }
             bool hit = LONGEST ? (STORE == STORE_VCS ? grid_longest_vcs<true>(o, d, reg, cr, dummy)
                                                      : grid_longest<true>(o, d, reg, cr, dummy))
@@ -1417,7 +1409,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             if (aborted) return false;
             if (hit) return true;
             advance_region(cr, o);
-            if (kExact && this->same_pos(cr, o, cr0, o0)) { aborted = true; return false; }
+            if (kExact && this->cycle_step(cyc, cr, o)) { aborted = true; return false; }
         }
         return false;
     }
@@ -1434,6 +1426,15 @@ __device__ __forceinline__ bool pixel_ray(const KView& v, uint32_t x, uint32_t l
     const uint32_t band = q0 + (up ? 1u : 0u), in_band = up ? r0 - v.band_rows : r0;
     const uint32_t y = v.row0 + (band * v.nranks + v.rank) * v.band_rows + in_band;
     if (y >= v.row_limit) return false;
+    if (v.tile_cols) {
+        // 2-D tile deal (uniform branch): local column -> frame column (vr_internal.h KView)
+        const uint32_t j0 = __umulhi(x, v.tile_minv), r1 = x - j0 * v.tile_cols;
+        const bool up1 = r1 >= v.tile_cols;
+        const uint32_t j = j0 + (up1 ? 1u : 0u), in_blk = up1 ? r1 - v.tile_cols : r1;
+        const uint32_t off = (v.col_rank + v.col_R - (v.col_stride * (band % v.col_R)) % v.col_R) % v.col_R;
+        x = (j * v.col_R + off) * v.tile_cols + in_blk;
+        if (x >= v.W) return false;
+    }
     if (!FAST) {
         float u = ((float)x + 0.5f) / (float)v.W;
         float vv = ((float)(v.H - y) + 0.5f) / (float)v.H;
@@ -1495,19 +1496,14 @@ __device__ __forceinline__ uint32_t defer_rewalk(const KView& v, uint32_t x, uin
     return kDeferMarker;
 }
 
-// The crawl pass's LDS for one record lane: its bit slot (per-record mode) or the
-// workgroup's copy of the scene's region table and cluster bits (scene-cached mode).
+// The crawl pass's LDS for one record lane: its cluster-bit slot.
 struct CrawlLds {
     uint32_t* lbm = nullptr;
-    const uint32_t* lrt = nullptr;
-    const uint32_t* lbits = nullptr;
 };
 template <class W>
 __device__ __forceinline__ void attach(W& w, const CrawlLds* cl) {
     if (!cl) return;
     w.lbm = cl->lbm;
-    w.lrt = cl->lrt;
-    w.lbits = cl->lbits;
 }
 
 // The body of rayMarchSceneOriginal / rayMarchSceneJumpAxis (Renderer.cuh:1033-1063)
@@ -1519,11 +1515,11 @@ __device__ __forceinline__ void attach(W& w, const CrawlLds* cl) {
 // the oracle.
 template <int STORE, int ALGO, bool COUNT, bool CRAWL>
 __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint32_t x, uint32_t l,
-                                          uint32_t& bytes, uint32_t* iters = nullptr, uint32_t* ff = nullptr,
+                                          uint32_t& bytes, uint32_t* iters = nullptr, uint2* ff = nullptr,
                                           uint32_t* dg = nullptr, const CrawlLds* cl = nullptr) {
     uint32_t col = 0;
     bytes = 0;
-    if (ff) *ff = 0;
+    if (ff) *ff = uint2{0u, 0u};
     f3 ro, rd;
     if (pixel_ray<true>(v, x, l, ro, rd)) {
         Walker<STORE, COUNT, CRAWL> w(s, v);
@@ -1532,13 +1528,13 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
         if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
         if (iters) *iters = w.iters;              // the walk's length (the work order's cost)
         bytes = w.bytes + 4u;                     // + the pixel write
-        if (ff) *ff = w.ff;
+        if (ff) *ff = uint2{w.ff, w.nl};
 #ifdef VR_CRAWL_PROF
         if (dg) { dg[0] = w.iters - w.ff; dg[1] = w.d_runs; dg[2] = w.d_trips; }
 #endif
         if (w.aborted) {
             col = 0;
-            if (ff) *ff = 0;
+            if (ff) *ff = uint2{0u, 0u};
             if (Walker<STORE, COUNT, CRAWL>::kExact) {
                 bytes = 4u;
             } else {
@@ -1554,7 +1550,7 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
 // finished from there (its iterations and bytes so far are the record's).
 template <int STORE, int ALGO, bool COUNT>
 __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v,
-                                                 const uint32_t* r, uint32_t& bytes, uint32_t& ff,
+                                                 const uint32_t* r, uint32_t& bytes, uint2& ff,
                                                  uint32_t* dg = nullptr, const CrawlLds* cl = nullptr) {
     const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
     Walker<STORE, COUNT, true> w(s, v);
@@ -1577,14 +1573,14 @@ __device__ __forceinline__ uint32_t shade_resume(const KScene& s, const KView& v
         col = r[18] * (uint32_t)!sh;
     }
     bytes = w.bytes + 4u;
-    ff = w.ff;
+    ff = uint2{w.ff, w.nl};
 #ifdef VR_CRAWL_PROF
     if (dg) { dg[0] = w.iters - r[9] - w.ff; dg[1] = w.d_runs; dg[2] = w.d_trips; }
 #endif
     if (w.aborted) {                              // never finishes (see shade)
         col = 0;
         bytes = 4u;
-        ff = 0;
+        ff = uint2{0u, 0u};
     }
     return col;
 }
@@ -1593,12 +1589,16 @@ __device__ __forceinline__ void add_bytes(const KView& v, uint32_t lane, unsigne
     for (int off = 32; off > 0; off >>= 1) b += __shfl_down(b, off, 64);   // one atomic per wave
     if (lane == 0 && b) atomicAdd(v.bytes, b);
 }
-// the crawl pass's fast-forwarded iterations (KView::stats)
-__device__ __forceinline__ void add_ff(const KView& v, uint32_t lane, unsigned long long n) {
-    for (int off = 32; off > 0; off >>= 1) n += __shfl_down(n, off, 64);
-    if (lane == 0 && n && v.stats) {
+// the crawl pass's existence reads credited without a load (KView::stats): n crawl
+// iterations fast-forwarded in closed form, m skip steps answered from the LDS cluster bits
+__device__ __forceinline__ void add_ff(const KView& v, uint32_t lane, unsigned long long n, unsigned long long m) {
+    for (int off = 32; off > 0; off >>= 1) {
+        n += __shfl_down(n, off, 64);
+        m += __shfl_down(m, off, 64);
+    }
+    if (lane == 0 && (n | m) && v.stats) {
         atomicAdd(v.stats, n);
-        atomicAdd(v.stats + 1, 4ull * n);
+        atomicAdd(v.stats + 1, 4ull * (n + m));
     }
 }
 
@@ -1634,10 +1634,10 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, (TileWaves<ALGO, HI>::value
     const uint32_t x = (bx * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
     const uint32_t l = (by * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
     uint32_t bytes = 0, iters = 0;
-    if (x < v.W && l < v.local_rows) {
+    if (x < v.LW && l < v.local_rows) {
         // (&iters unconditionally: a pointer chosen by `v.cost ? &iters : nullptr` keeps
         // iters in scratch -- a store and a reload per lane, 8 MB of WRITE_SIZE per C2 launch)
-        v.out[(size_t)l * v.W + x] = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes, &iters);
+        v.out[(size_t)l * v.LW + x] = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes, &iters);
     }
     if (COUNT) add_bytes(v, lane, bytes);
     if (v.cost) {                                  // the wave's walk length, for the next work order
@@ -1685,21 +1685,17 @@ __global__ __launch_bounds__(1024) void order_kernel(const uint32_t* __restrict_
 #endif
 constexpr uint32_t kCrawlRpw = VR_CRAWL_RPW;
 constexpr uint32_t kCrawlMaxRpw = 16;     // records per wave with an LDS bitmap slot
-// Workgroup shapes: per-record mode 2 waves (as the tile pass); scene-cached mode 8 waves,
-// one workgroup per CU (its LDS copy of the scene is up to kCrawlSceneLdsMax bytes).
-constexpr uint32_t kCrawlWaves = 2, kCrawlSceneWaves = 8;
-constexpr uint32_t kCrawlSceneLdsMax = 144u * 1024u;
-// Dynamic LDS layout (16-B aligned carve-outs, cdna_hip_programming.md Guideline 17):
-//   [0, 16)        record count, overflow count
-//   per-record:    16 words per record lane (kCrawlMaxRpw per wave)
-//   scene-cached:  the region table (D^3 words, padded to 16 B), then every region's 16
-//                  cluster-bit words
-__device__ __forceinline__ uint32_t rt_words_padded(const KScene& s) {
-    return ((s.D * s.D * s.D) + 3u) & ~3u;
-}
+// Workgroup shape: 2 waves (as the tile pass).  (Round 4 measured an opt-in mode that cached
+// the scene's whole region table and cluster bits in each 8-wave workgroup's LDS: no faster
+// alone, slower in flight, profiles/r04/crawl/scene_lds_ab.txt -- removed in round 5.)
+constexpr uint32_t kCrawlWaves = 2;
+// LDS (16-B aligned carve-outs, cdna_hip_programming.md Guideline 17):
+//   [0, 16)   record count, overflow count
+//   then      16 words (a region's cluster-existence bits) per record lane, kCrawlMaxRpw per wave
+constexpr uint32_t kCrawlLdsWords = 4u + kCrawlWaves * kCrawlMaxRpw * 16u;
 template <int STORE, int ALGO, bool COUNT>
-__global__ __launch_bounds__(64 * kCrawlSceneWaves) void crawl_kernel(KScene s, KView v) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+__global__ __launch_bounds__(64 * kCrawlWaves) void crawl_kernel(KScene s, KView v) {
+    __shared__ __attribute__((aligned(16))) uint32_t dyn[kCrawlLdsWords];
     if (threadIdx.x == 0) {
         dyn[0] = v.defer[0];
         dyn[1] = v.defer[2];
@@ -1711,19 +1707,7 @@ __global__ __launch_bounds__(64 * kCrawlSceneWaves) void crawl_kernel(KScene s, 
     if (total == 0u && overflow == 0u) return;   // nothing deferred (the usual case): no reset needed
     const uint32_t n = min(total, v.defer_cap);
     CrawlLds cl;
-    if (STORE == STORE_VCS && v.crawl_scene_lds) {
-        // the scene's region table and cluster bits, once per workgroup: a record's walk then
-        // reads global memory only for present clusters' mask words and the hit's colour
-        const uint32_t nrt = s.D * s.D * s.D, off = 4u + rt_words_padded(s), nb = s.n_regions * 16u;
-        for (uint32_t i = threadIdx.x; i < nrt; i += blockDim.x) dyn[4 + i] = s.region_slot[i];
-        const uint4* src = reinterpret_cast<const uint4*>(s.vcs_cbits);
-        uint4* dst = reinterpret_cast<uint4*>(dyn + off);
-        for (uint32_t i = threadIdx.x; i < nb / 4u; i += blockDim.x) dst[i] = src[i];
-        __syncthreads();
-        cl.lrt = dyn + 4;
-        cl.lbits = dyn + off;
-    }
-    unsigned long long bytes = 0, ffs = 0;
+    unsigned long long bytes = 0, ffs = 0, nls = 0;
     // kCrawlRpw records per wave at a time (lanes 0 .. kCrawlRpw-1): each record is a long
     // chain of dependent iterations, and the lanes of a wave take different paths through
     // the walk, so fewer lanes per wave -- spread over more waves -- finish sooner
@@ -1733,8 +1717,7 @@ __global__ __launch_bounds__(64 * kCrawlSceneWaves) void crawl_kernel(KScene s, 
     const uint32_t rpw = v.crawl_rpw ? v.crawl_rpw : kCrawlRpw;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, wlane = threadIdx.x & 63u;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    if (STORE == STORE_VCS && !v.crawl_scene_lds && s.vcs_cbits && rpw <= kCrawlMaxRpw && wlane < rpw &&
-        blockDim.x <= 64u * kCrawlWaves)
+    if (STORE == STORE_VCS && s.vcs_cbits && rpw <= kCrawlMaxRpw && wlane < rpw)
         cl.lbm = dyn + 4 + ((threadIdx.x >> 6) * kCrawlMaxRpw + wlane) * 16u;
     for (uint32_t i = wave * rpw + wlane; wlane < rpw && i < n; i += nwaves * rpw) {
         uint32_t* r = v.defer + 4 + (size_t)i * kDeferRecWords;
@@ -1759,11 +1742,11 @@ __global__ __launch_bounds__(64 * kCrawlSceneWaves) void crawl_kernel(KScene s, 
                 r[15 + a] = (uint32_t)qa;
             }
         }
-        uint32_t f = 0;
+        uint2 f{0u, 0u};
 #ifdef VR_CRAWL_PROF
         uint32_t dg[3] = {0, 0, 0};
         const long long c0 = clock64(), t0 = wall_clock64();
-        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, dg, &cl)
+        v.out[(size_t)l * v.LW + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, dg, &cl)
                                          : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f, dg, &cl);
         const long long c1 = clock64(), t1 = wall_clock64();
         if (i < 16384u) {
@@ -1775,32 +1758,32 @@ __global__ __launch_bounds__(64 * kCrawlSceneWaves) void crawl_kernel(KScene s, 
             g_vr_crawl_prof[8 * i + 5] = (uint32_t)t1;
         }
 #else
-        v.out[(size_t)l * v.W + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, nullptr, &cl)
+        v.out[(size_t)l * v.LW + x] = amb ? shade<STORE, ALGO, COUNT, true>(s, v, x, l, b, nullptr, &f, nullptr, &cl)
                                          : shade_resume<STORE, ALGO, COUNT>(s, v, r, b, f, nullptr, &cl);
 #endif
         bytes += b;
-        ffs += f;
+        ffs += f.x;
+        nls += f.y;
     }
     if (overflow != 0u) {
         // the list overflowed: the pixels the tile pass could not defer carry the marker
-        const size_t npx = (size_t)v.local_rows * v.W;
+        const size_t npx = (size_t)v.local_rows * v.LW;
         for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (size_t)gridDim.x * blockDim.x) {
             if (v.out[i] != kDeferMarker) continue;
-            uint32_t b, f = 0;
-            // (the scene-cached LDS is the workgroup's: usable by every lane; a per-record bit
-            // slot is not this lane's)
-            CrawlLds clo;
-            clo.lrt = cl.lrt;
-            clo.lbits = cl.lbits;
-            v.out[i] = shade<STORE, ALGO, COUNT, true>(s, v, (uint32_t)(i % v.W), (uint32_t)(i / v.W), b, nullptr, &f,
+            uint32_t b;
+            uint2 f{0u, 0u};
+            // (a per-record bit slot is not this lane's: none)
+            const CrawlLds clo;
+            v.out[i] = shade<STORE, ALGO, COUNT, true>(s, v, (uint32_t)(i % v.LW), (uint32_t)(i / v.LW), b, nullptr, &f,
                                                        nullptr, &clo);
             bytes += b;
-            ffs += f;
+            ffs += f.x;
+            nls += f.y;
         }
     }
     if (COUNT) {
         add_bytes(v, threadIdx.x & 63u, bytes);
-        add_ff(v, threadIdx.x & 63u, ffs);
+        add_ff(v, threadIdx.x & 63u, ffs, nls);
     }
     // Every workgroup has read the count (above) before it adds to `done`; the
     // last one clears the slot for its next launch (ordered by the kernel boundary).
@@ -1832,6 +1815,22 @@ __global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __rest
     rgb[3 * i + 2] = (uint8_t)(c & 0xFFu);
 }
 
+// Rank 0's reassembly of the 2-D tile deal (vr_internal.h TileLayout): one thread per frame
+// pixel reads its owner's local pixel -- the inverse of pixel_ray's column map -- and copies
+// E bytes.  (The gathered buffers are read once and the frame written once: HBM-bound.)
+template <int E>
+__global__ void assemble_tiles_kernel(const uint8_t* __restrict__ parts, uint8_t* __restrict__ frame, TileLayout t) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)t.W * t.H) return;
+    const uint32_t y = (uint32_t)(i / t.W), x = (uint32_t)(i - (uint64_t)y * t.W);
+    const uint32_t b = y / t.band_rows, j = x / t.tile_cols, in_blk = x - j * t.tile_cols;
+    const uint32_t rank = (j + t.stride * (b % t.R)) % t.R;
+    const uint64_t lx = (uint64_t)(j / t.R) * t.tile_cols + in_blk;
+    const uint64_t src = (uint64_t)rank * t.rank_words + (uint64_t)y * t.LW + lx;
+#pragma unroll
+    for (int k = 0; k < E; ++k) frame[i * E + k] = parts[src * E + k];
+}
+
 }  // namespace
 
 // The tile pass, then the crawl pass (a small grid that exits at once when nothing
@@ -1843,23 +1842,6 @@ __global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __rest
 // flight, profiles/r03/ab_crawl_rpw.txt), at least 64 workgroups.  The host sizes it from
 // the count an earlier launch of the device wrote to defer_stat: a launch that defers
 // nothing (C2-C4) keeps the small grid (1024 empty workgroups cost C2 0.6 %).
-uint32_t crawl_threads(bool scene_lds) { return 64u * (scene_lds ? kCrawlSceneWaves : kCrawlWaves); }
-uint32_t crawl_lds_bytes(const KScene& s, bool scene_lds) {
-    if (!scene_lds) return 16u + kCrawlWaves * kCrawlMaxRpw * 16u * 4u;
-    const uint64_t nrt = (uint64_t)s.D * s.D * s.D;
-    return (uint32_t)std::min<uint64_t>(16u + 4u * (((nrt + 3u) & ~3ull) + (uint64_t)s.n_regions * 16u), 0xFFFFFFFFu);
-}
-bool crawl_lds_fits(const KScene& s) {
-    const uint64_t nrt = (uint64_t)s.D * s.D * s.D;
-    return s.vcs_cbits && 16u + 4u * (((nrt + 3u) & ~3ull) + (uint64_t)s.n_regions * 16u) <= kCrawlSceneLdsMax;
-}
-// scene-cached mode: one 8-wave workgroup per CU holds rpw records per wave; waves loop over
-// further records when there are more than 256 workgroups' worth
-uint32_t crawl_grid_scene_lds(uint32_t records, uint32_t rpw) {
-    rpw = rpw ? rpw : kCrawlRpw;
-    const uint64_t per = (uint64_t)kCrawlSceneWaves * rpw;
-    return (uint32_t)std::min<uint64_t>(std::max<uint64_t>((records + per - 1) / per, 1u), 256u);
-}
 uint32_t crawl_grid(uint32_t records, uint32_t rpw) {
     const uint32_t waves_per_wg = kCrawlWaves;
     rpw = rpw ? rpw : kCrawlRpw;
@@ -1878,7 +1860,7 @@ constexpr bool kNoCrawlPass = false;
 #endif
 
 void march_grid(const KView& v, uint32_t& columns, uint32_t& rows) {
-    columns = (v.W + 8u * kTilesX - 1u) / (8u * kTilesX);
+    columns = (v.LW + 8u * kTilesX - 1u) / (8u * kTilesX);
     rows = (v.local_rows + 8u * kTilesY - 1u) / (8u * kTilesY);
 }
 
@@ -1896,20 +1878,13 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
     dim3 block(64u * kTilesX * kTilesY);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     const dim3 cgrid(crawl_wgs ? crawl_wgs : 64u);
-    const bool scene_lds = v.crawl_scene_lds != 0;
-    const dim3 cblock(crawl_threads(scene_lds));
-    const uint32_t clds = crawl_lds_bytes(s, scene_lds);
+    const dim3 cblock(64u * kCrawlWaves);
 #define VR_LAUNCH(ST, AL, CT) VR_LAUNCH_HI(ST, AL, CT, false)
 #define VR_LAUNCH_HI(ST, AL, CT, HI)                                                              \
     do {                                                                                           \
         hipLaunchKernelGGL((march_kernel<ST, AL, CT, HI>), grid, block, 0, stream, s, v);          \
-        if (v.defer && !kNoCrawlPass) {                                                            \
-            static const hipError_t attr = hipFuncSetAttribute(                                    \
-                reinterpret_cast<const void*>(&crawl_kernel<ST, AL, CT>),                          \
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCrawlSceneLdsMax);                \
-            if (attr != hipSuccess) return attr;                                                   \
-            hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, cblock, clds, stream, s, v);     \
-        }                                                                                          \
+        if (v.defer && !kNoCrawlPass)                                                              \
+            hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, cblock, 0, stream, s, v);        \
     } while (0)
 #ifdef VR_ISA_ONLY
     // ISA-inspection builds (csrc/Makefile isa1, profiles/loop_isa.py): one kernel pair
@@ -1943,6 +1918,22 @@ hipError_t launch_cluster_bits(const uint2* vcs_mask, uint32_t n_regions, uint32
     const uint32_t threads = n_regions * 16u;
     hipLaunchKernelGGL(cluster_bits_kernel, dim3((threads + 255u) / 256u), dim3(256), 0, stream, vcs_mask, n_regions,
                        cbits);
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble_tiles(const void* parts, void* frame, uint32_t elem_bytes, const TileLayout& t,
+                                 hipStream_t stream) {
+    const uint64_t n = (uint64_t)t.W * t.H;
+    if (n == 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    const uint8_t* p = static_cast<const uint8_t*>(parts);
+    uint8_t* f = static_cast<uint8_t*>(frame);
+    switch (elem_bytes) {
+    case 1: hipLaunchKernelGGL(assemble_tiles_kernel<1>, grid, block, 0, stream, p, f, t); break;
+    case 2: hipLaunchKernelGGL(assemble_tiles_kernel<2>, grid, block, 0, stream, p, f, t); break;
+    case 3: hipLaunchKernelGGL(assemble_tiles_kernel<3>, grid, block, 0, stream, p, f, t); break;
+    default: hipLaunchKernelGGL(assemble_tiles_kernel<4>, grid, block, 0, stream, p, f, t); break;
+    }
     return hipGetLastError();
 }
 

@@ -271,20 +271,34 @@ class Schedule(enum.IntEnum):
     HEAVIEST_FIRST = _capi.VR_SCHEDULE_HEAVIEST_FIRST
 
 
+class Occupancy(enum.IntEnum):
+    """vr_occupancy: the tile pass's occupancy variant (identical pixels).  AUTO: the in-flight
+    variant (cuckoo original 8 waves/SIMD, VCS longest axis 7) while another stream's launch runs."""
+    AUTO = _capi.VR_OCCUPANCY_AUTO
+    LONE = _capi.VR_OCCUPANCY_LONE
+    IN_FLIGHT = _capi.VR_OCCUPANCY_IN_FLIGHT
+
+
 def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
               info: VoxelSceneInfo, width: int, height: int, out: torch.Tensor, row_begin: int = 0,
               row_end: int | None = None, band_rows: int = 0, rank: int = 0, nranks: int = 1,
               counter: torch.Tensor | None = None, kernel: Kernel = Kernel.AUTO, stream=None,
               defer_cap: int = 0, schedule: Schedule = Schedule.AUTO,
-              stats: torch.Tensor | None = None) -> torch.Tensor:
+              stats: torch.Tensor | None = None, occupancy: Occupancy = Occupancy.AUTO,
+              tile_cols: int = 0, deal_stride: int = 0) -> torch.Tensor:
     """vr_render_ex: rows [row_begin,row_end), bands of band_rows (0 = one band) dealt to nranks ranks.
     defer_cap: capacity of the crawl pass's deferral list (0 = default; small values force its overflow path).
-    schedule: the tile pass's work order (Schedule).
+    schedule: the tile pass's work order (Schedule); occupancy: its occupancy variant (Occupancy).
     stats (with counter): CUDA int64[2], caller-zeroed: [0] crawl iterations fast-forwarded in closed form,
-    [1] the existence-read bytes credited for them (part of counter's count, never loaded)."""
+    [1] the existence-read bytes credited for them (part of counter's count, never loaded).
+    tile_cols > 0: the 2-D tile deal (block j of band b -> rank (j + deal_stride * b) % nranks;
+    tile_buffer_words per rank)."""
     row_end = height if row_end is None else row_end
     rows = row_end - row_begin
-    words = band_buffer_words(width, rows, band_rows or max(1, rows), nranks)
+    if tile_cols:
+        words = tile_buffer_words(width, rows, band_rows or max(1, rows), tile_cols, nranks)
+    else:
+        words = band_buffer_words(width, rows, band_rows or max(1, rows), nranks)
     _require_u32(out, words)
     for name, t in (("counter", counter), ("stats", stats)):
         if t is not None and (not t.is_cuda or t.dtype != torch.int64):
@@ -298,6 +312,7 @@ def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, 
     opts.bytes_dev = c_void_p(counter.data_ptr()) if counter is not None else None
     opts.defer_cap, opts.schedule = int(defer_cap), int(schedule)
     opts.stats_dev = c_void_p(stats.data_ptr()) if stats is not None else None
+    opts.occupancy, opts.tile_cols, opts.deal_stride = int(occupancy), int(tile_cols), int(deal_stride)
     check(lib().vr_render_ex(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
                              f3(info.translation), int(info.scale), int(width), int(height), ctypes.byref(opts),
                              c_void_p(out.data_ptr()), _stream_ptr(stream)), "vr_render_ex")
@@ -346,6 +361,41 @@ def render_bands(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camer
                                 int(rank), int(nranks), c_void_p(out.data_ptr()), _stream_ptr(stream)),
           "vr_render_bands")
     return out
+
+
+def tile_buffer_words(width: int, height: int, band_rows: int, tile_cols: int, nranks: int) -> int:
+    return int(lib().vr_tile_buffer_words(width, height, band_rows, tile_cols, nranks))
+
+
+def deal_stride_default(nranks: int) -> int:
+    return int(lib().vr_deal_stride_default(nranks))
+
+
+def render_tiles(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
+                 info: VoxelSceneInfo, width: int, height: int, band_rows: int, tile_cols: int, rank: int,
+                 nranks: int, out: torch.Tensor, stream=None) -> torch.Tensor:
+    """This rank's tiles of the 2-D deal (block j of band b -> rank (j + stride * b) % nranks), packed."""
+    _require_u32(out, tile_buffer_words(width, height, band_rows, tile_cols, nranks))
+    check(lib().vr_render_tiles(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
+                                f3(info.translation), int(info.scale), int(width), int(height), int(band_rows),
+                                int(tile_cols), int(rank), int(nranks), c_void_p(out.data_ptr()),
+                                _stream_ptr(stream)), "vr_render_tiles")
+    return out
+
+
+def assemble_tiles_device(parts: torch.Tensor, frame: torch.Tensor, elem_bytes: int, width: int, height: int,
+                          band_rows: int, tile_cols: int, nranks: int, deal_stride: int = 0,
+                          stream=None) -> torch.Tensor:
+    """vr_assemble_tiles: rank 0's reassembly on the device.  parts: the nranks tile buffers back to back
+    (contiguous, elem_bytes per pixel); frame: width x height pixels of elem_bytes (contiguous)."""
+    need = tile_buffer_words(width, height, band_rows, tile_cols, nranks) * nranks * elem_bytes
+    for name, t, n in (("parts", parts, need), ("frame", frame, width * height * elem_bytes)):
+        if not t.is_cuda or not t.is_contiguous() or t.numel() * t.element_size() < n:
+            raise ValueError(f"{name} must be a contiguous CUDA tensor of >= {n} bytes")
+    check(lib().vr_assemble_tiles(c_void_p(parts.data_ptr()), c_void_p(frame.data_ptr()), int(elem_bytes),
+                                  int(width), int(height), int(band_rows), int(tile_cols), int(nranks),
+                                  int(deal_stride), _stream_ptr(stream)), "vr_assemble_tiles")
+    return frame
 
 
 def pack_rgb8(words: torch.Tensor, stream=None, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -1,7 +1,12 @@
-"""Multi-GPU image tiling: interleaved row bands (band b -> rank b % R) and
-their reassembly after the gather.  SURVEY.md 8(e): pixels are independent,
-the voxel store is replicated per GPU, and the only exchange is the final
-gather of the framebuffer to rank 0.
+"""Multi-GPU image tiling and reassembly after the gather.  SURVEY.md 8(e): pixels are
+independent, the voxel store is replicated per GPU, and the only exchange is the final
+gather of the framebuffer to rank 0.  Two layouts (include/vr.h):
+
+  row bands -- band b of band_rows rows -> rank b % R (vr_render_bands);
+  2-D tiles -- every band cut into column blocks of tile_cols pixels, block j of band b ->
+               rank (j + stride * b) % R (vr_render_tiles): every rank gets a share of every
+               band, so a cluster of expensive rows (C5's crawl rows) is spread over all ranks
+               while each 8x8 wave tile stays whole.
 """
 from __future__ import annotations
 
@@ -27,6 +32,63 @@ def assemble_bands(parts: torch.Tensor, width: int, height: int, band_rows: int)
         raise ValueError(f"band buffers have {parts.shape[1]} words, expected {expect}")
     img = parts.reshape(R, per, band_rows, width).permute(1, 0, 2, 3).reshape(per * R * band_rows, width)
     return img[:height]
+
+
+def deal_stride(nranks: int, stride: int = 0) -> int:
+    """The 2-D deal's stride as the library uses it (vr_deal_stride_default for 0)."""
+    s = stride or (1 if nranks % 3 == 0 else 3)
+    return s % nranks
+
+
+def tile_local_width(width: int, tile_cols: int, nranks: int) -> int:
+    """Words per local row of a 2-D tile buffer: this rank's column blocks of one band."""
+    nblk = -(-width // tile_cols)
+    return -(-nblk // nranks) * tile_cols
+
+
+def tile_words(width: int, height: int, band_rows: int, tile_cols: int, nranks: int) -> int:
+    """vr_tile_buffer_words (the same arithmetic, without the library)."""
+    return -(-height // band_rows) * band_rows * tile_local_width(width, tile_cols, nranks)
+
+
+def tile_source_index(width: int, height: int, band_rows: int, tile_cols: int, nranks: int,
+                      stride: int = 0) -> torch.Tensor:
+    """For every frame pixel (row-major), its index in the nranks tile buffers laid back to back:
+    the inverse of the 2-D deal (vr_internal.h KView, vr_march.hip assemble_tiles_kernel)."""
+    s = deal_stride(nranks, stride)
+    words = tile_words(width, height, band_rows, tile_cols, nranks)
+    lw = tile_local_width(width, tile_cols, nranks)
+    y = torch.arange(height, dtype=torch.int64)[:, None]
+    x = torch.arange(width, dtype=torch.int64)[None, :]
+    b, j = y // band_rows, x // tile_cols
+    rank = (j + s * (b % nranks)) % nranks
+    lx = (j // nranks) * tile_cols + x % tile_cols
+    return (rank * words + y * lw + lx).reshape(-1)
+
+
+def assemble_tiles(parts: torch.Tensor, width: int, height: int, band_rows: int, tile_cols: int,
+                   stride: int = 0) -> torch.Tensor:
+    """parts: [R, words * px] per-rank tile buffers (px elements per pixel) -> [height, width * px].
+    (Host-side form for CPU tests; rank 0 on a GPU uses vr_assemble_tiles.)"""
+    R = parts.shape[0]
+    words = tile_words(width, height, band_rows, tile_cols, R)
+    px, rem = divmod(parts.shape[1], words)
+    if rem or px < 1:
+        raise ValueError(f"tile buffers have {parts.shape[1]} elements, expected a multiple of {words}")
+    idx = tile_source_index(width, height, band_rows, tile_cols, R, stride).to(parts.device)
+    return parts.reshape(R * words, px).index_select(0, idx).reshape(height, width * px)
+
+
+def tile_rank_buffer(frame: torch.Tensor, rank: int, nranks: int, band_rows: int, tile_cols: int,
+                     stride: int = 0) -> torch.Tensor:
+    """What rank `rank` renders of `frame` [H, W] in the 2-D deal (0 past the frame): for tests."""
+    H, W = frame.shape
+    words = tile_words(W, H, band_rows, tile_cols, nranks)
+    idx = tile_source_index(W, H, band_rows, tile_cols, nranks, stride)
+    mine = (idx // words) == rank
+    buf = torch.zeros(words, dtype=frame.dtype)
+    buf[idx[mine] - rank * words] = frame.reshape(-1)[mine]
+    return buf
 
 
 def owned_rows(height: int, band_rows: int, rank: int, nranks: int) -> list[int]:
@@ -69,13 +131,15 @@ def pipeline_hw_queues(depth: int, nranks: int = 1) -> int:
     return 16 if streams > 4 else 0
 
 
-def init_frame_group(world: int, local_rank: int, backend: str = "auto", same_device: bool = False):
+def init_frame_group(world: int, local_rank: int, backend: str = "auto", same_device: bool = False,
+                     force_group: bool = False):
     """The device and process group of one rank of the frame pipeline (bench.py's N > 1
     path).  backend "auto"/"nccl": RCCL over xGMI, one GPU per rank (RCCL refuses two ranks
     on one device).  "gloo": the same pipeline with the gather staged through host memory
     (BandGather(stage_host=True)) -- what lets N ranks share one GPU (same_device: every
     rank on cuda:0) to run the multi-rank path on a one-GPU box.
-    Returns (device, backend, stage_host); world == 1 starts no group."""
+    Returns (device, backend, stage_host); world == 1 starts no group unless force_group
+    (bench.py --exchange: one rank through the whole N > 1 path, RCCL included)."""
     import torch.distributed as dist
     dev_index = 0 if same_device else local_rank
     torch.cuda.set_device(dev_index)
@@ -86,7 +150,7 @@ def init_frame_group(world: int, local_rank: int, backend: str = "auto", same_de
         raise ValueError(f"unknown backend {backend!r}")
     if same_device and world > 1 and backend == "nccl":
         raise ValueError("several ranks on one GPU need the gloo backend (RCCL refuses a duplicate GPU)")
-    if world > 1:
+    if world > 1 or force_group:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -103,7 +167,8 @@ def weak_scaled_resolution(width: int, height: int, nranks: int) -> tuple[int, i
 
 
 class BandGather:
-    """Row-band image tiling across ranks, with frames in flight.
+    """Image tiling across ranks (row bands, or the 2-D tile deal with tile_cols > 0), with
+    frames in flight.
 
     step(render) renders this rank's bands of the next frame into one of `depth`
     band buffers and starts an asynchronous gather of it to rank 0 (RCCL on
@@ -119,32 +184,43 @@ class BandGather:
     """
 
     def __init__(self, width: int, height: int, band_rows: int, rank: int, nranks: int,
-                 device, depth: int = 2, on_frame=None, rgb8: bool = False, stage_host: bool = False):
+                 device, depth: int = 2, on_frame=None, rgb8: bool = False, stage_host: bool = False,
+                 tile_cols: int = 0, stride: int = 0, exchange: bool | None = None):
         self.W, self.H, self.B = width, height, band_rows
         self.rank, self.R, self.depth = rank, nranks, depth
-        words = band_buffer_words(width, height, band_rows, nranks)
+        # exchange: gather every frame to rank 0 and assemble it there (N > 1; with one rank it
+        # is forced only to run that code -- RCCL included -- on a one-GPU box)
+        self.x = nranks > 1 if exchange is None else bool(exchange)
+        x = self.x
+        # the 2-D tile deal (with the exchange only: without it the band buffer is the frame)
+        self.T = int(tile_cols) if x else 0
+        self.stride = deal_stride(nranks, stride) if self.T else 0
+        words = (tile_words(width, height, band_rows, self.T, nranks) if self.T else
+                 band_buffer_words(width, height, band_rows, nranks))
+        self.words = words
         self.per = bands_per_rank(height, band_rows, nranks)
         self.bufs = [torch.empty(words, dtype=torch.int32, device=device) for _ in range(depth)]
         # rgb8 (GPUs, N > 1): the bands travel as the RGB8 framebuffer (3 B per pixel
         # instead of the 4-B packed word: a quarter less over xGMI) and rank 0
         # assembles an RGB8 frame [H, W, 3]
-        self.rgb8 = bool(rgb8) and nranks > 1
+        self.rgb8 = bool(rgb8) and x
         self.px = 3 if self.rgb8 else 1                  # elements per pixel in the exchanged buffers
         xdt = torch.uint8 if self.rgb8 else torch.int32
         self.packed = ([torch.empty(words * 3, dtype=torch.uint8, device=device) for _ in range(depth)]
                        if self.rgb8 else None)
         self.recv = ([torch.empty((nranks, words * self.px), dtype=xdt, device=device) for _ in range(depth)]
-                     if (rank == 0 and nranks > 1) else None)
+                     if (rank == 0 and x) else None)
         # stage_host (a gloo group over GPU buffers -- gloo gathers host tensors only, e.g.
         # several ranks sharing one GPU, where RCCL refuses): each frame's send buffer is
         # copied to pinned host memory once its render is complete, gathered there, and the
         # receive buffers are copied back to the device before the same assembly
-        self.stage = bool(stage_host) and nranks > 1 and torch.device(device).type == "cuda"
+        self.stage = bool(stage_host) and x and torch.device(device).type == "cuda"
         if self.stage:
             self.h_send = [torch.empty(words * self.px, dtype=xdt, pin_memory=True) for _ in range(depth)]
             self.h_recv = ([torch.empty((nranks, words * self.px), dtype=xdt, pin_memory=True) for _ in range(depth)]
                            if rank == 0 else None)
-        self.frame = (torch.empty((self.per * nranks * band_rows, width * self.px), dtype=xdt, device=device)
+        frame_rows = height if self.T else self.per * nranks * band_rows
+        self.frame = (torch.empty((frame_rows, width * self.px), dtype=xdt, device=device)
                       if rank == 0 else None)
         self.work = [None] * depth
         dev = torch.device(device)
@@ -153,7 +229,7 @@ class BandGather:
         # rank 0: the un-interleaving copy on a side stream (the render is latency-bound,
         # the copy HBM-bound); a receive buffer is gathered into again only after its
         # copy has finished.
-        self.side = torch.cuda.Stream(dev) if (cuda and rank == 0 and nranks > 1) else None
+        self.side = torch.cuda.Stream(dev) if (cuda and rank == 0 and x) else None
         self.copied = [None] * depth
         self.pending = []            # slots in submission order
         self.on_frame = on_frame     # rank 0: callback(frame[:H]) after each assembled frame
@@ -165,18 +241,27 @@ class BandGather:
 
     def _assemble(self, slot: int) -> None:
         rw = self.W * self.px
-        src = self.recv[slot].view(self.R, self.per, self.B, rw).permute(1, 0, 2, 3)
-        self.frame.view(self.per, self.R, self.B, rw).copy_(src)
+        if self.T:
+            if self.recv[slot].is_cuda:                    # one un-dealing kernel (vr_assemble_tiles)
+                from .renderer import assemble_tiles_device
+                eb = self.px * self.recv[slot].element_size()
+                assemble_tiles_device(self.recv[slot], self.frame, eb, self.W, self.H, self.B, self.T, self.R,
+                                      self.stride)
+            else:
+                self.frame.copy_(assemble_tiles(self.recv[slot], self.W, self.H, self.B, self.T, self.stride))
+        else:
+            src = self.recv[slot].view(self.R, self.per, self.B, rw).permute(1, 0, 2, 3)
+            self.frame.view(self.per, self.R, self.B, rw).copy_(src)
         if self.on_frame is not None:
             f = self.frame[:self.H]
             self.on_frame(f.view(self.H, self.W, 3) if self.rgb8 else f)
 
     def _finish(self, slot: int) -> None:
-        if self.R == 1 and self.on_frame is None:     # nothing to hand over (the bench's loop)
+        if not self.x and self.on_frame is None:     # nothing to hand over (the bench's loop)
             self.pending.remove(slot)
             return
         with self._slot_stream(slot):
-            if self.R == 1:
+            if not self.x:
                 if self.on_frame is not None:
                     self.on_frame(self.bufs[slot].view(-1, self.W)[:self.H])
             else:
@@ -206,7 +291,7 @@ class BandGather:
             self.streams[slot].wait_stream(torch.cuda.current_stream()) if self.k < self.depth else None
         with self._slot_stream(slot):
             render(self.bufs[slot])
-            if self.R > 1:
+            if self.x:
                 import torch.distributed as dist
                 send = self.bufs[slot]
                 if self.rgb8:
@@ -231,7 +316,7 @@ class BandGather:
     def last_frame(self) -> torch.Tensor:
         """After drain(): rank 0's last frame -- [H, W, 3] uint8 RGB8 when the bands travel
         as RGB8, else [H, W] packed words (the band buffer itself with one rank)."""
-        if self.R == 1:
+        if not self.x:
             return self.bufs[self.last].view(-1, self.W)[:self.H]
         f = self.frame[:self.H]
         return f.view(self.H, self.W, 3) if self.rgb8 else f
