@@ -76,14 +76,16 @@ def test_device_build_errors():
 @pytest.mark.parametrize("build", [vr.Build.DEVICE, vr.Build.HOST], ids=["device", "host"])
 def test_vcs_region_limit(build):
     """VCS walks address cluster masks by a 32-bit byte offset (64 KB per occupied
-    region): a VCS scene may hold at most 65 536 occupied regions; more is an error,
-    the hash store has no such limit."""
+    region): a VCS scene may hold at most 65 536 occupied regions; more is an error.
+    The hash store has the same bound since round 5 (its key-presence filter is 32 KB per
+    occupied region, addressed the same way)."""
     g = np.arange(41, dtype=np.int32) * 64
     xyz = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)   # 68 921 regions
     rgb = np.full(len(xyz), 7, np.uint32)
-    with pytest.raises(vr.VrError) as e:
-        vr.create_scene(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE, build=build)
-    assert e.value.code == -1 and "65536" in str(e.value)
+    for store in (vr.StorageType.VOXEL_CLUSTER_STORE, vr.StorageType.HASH_TABLE):
+        with pytest.raises(vr.VrError) as e:
+            vr.create_scene(xyz, rgb, store, build=build)
+        assert e.value.code == -1 and "65536" in str(e.value)
     if build != vr.Build.DEVICE:
         return
     # the largest allowed scene (4 GB of masks) builds -- when the device has room for it
@@ -110,6 +112,16 @@ def test_vcs_region_limit(build):
         assert np.array_equal(got, want) and gb == wb
         assert np.count_nonzero(want) > 0          # the last region's voxel is hit
     ok.close()
+    # the hash store at the bound: its last region's filter at byte offset 65535 << 15
+    okh = vr.create_scene(xyz[:65536], rgb[:65536], vr.StorageType.HASH_TABLE, build=build)
+    assert okh.info()["region_count"] == 65536
+    refh = oracle.Scene(xyz[:65536], rgb[:65536], 1)
+    for algo in (vr.RayMarchAlgorithm.ORIGINAL, vr.RayMarchAlgorithm.LONGEST_AXIS):
+        want, wb = refh.render(int(algo), oracle_camera_from(cam), oracle_lighting_from(lit), 16, 16, 1)
+        got, gb = gpu_render(okh, algo, cam, lit, vr.VoxelSceneInfo((0.0, 0.0, 0.0), 1), 16, 16, count=True)
+        assert np.array_equal(got, want) and gb == wb
+        assert np.count_nonzero(want) > 0
+    okh.close()
 
 
 def test_device_built_scene_renders_like_oracle():

@@ -360,6 +360,16 @@ struct Ctx {
             return found ? s.vcs_vals[idx] : kEmpty;
         } else {
             const uint32_t key = ((uint32_t)x << 20) | ((uint32_t)y << 10) | (uint32_t)z;   // generate3DPoint
+            // the region's key-presence filter (KScene::ht_filter): a key the tables do not hold
+            // costs the reference key1 + key2 and misses.  Tables hold local keys only (fields
+            // x, y, z < 64), so a key with any other bit set -- a coordinate outside the
+            // region, wrapped into the 32-bit key -- cannot be there.
+            if ((key & ~0x03F0FC3Fu) != 0u) { count(8); return kEmpty; }
+            {
+                const uint32_t kx = (key >> 20) & 63u, ky = (key >> 10) & 63u, kz = key & 63u;
+                const uint32_t fw = s.ht_filter[(size_t)reg * kHashFilterWords + word_index(kx, ky, kz)];
+                if (!((fw >> (word_bit5(ky, kz) & 31u)) & 1u)) { count(8); return kEmpty; }
+            }
             const uint4 m = s.ht_meta[reg];          // {base, M, prime, offset}
             const uint32_t s1 = hash1(key, m.w) % m.y;
             const uint32_t s2 = hash2(key, m.z) % m.y;

@@ -139,8 +139,10 @@ struct vr_scene {
     uint64_t n_voxels = 0;
     DevBuf region_slot, vcs_mask, vcs_vals, ht_meta, ht_slots;
     DevBuf vcs_cbits;   // derived (not part of vr_scene_digest): cluster-existence bits per region
+    DevBuf ht_filter;   // derived (not part of vr_scene_digest): cuckoo key-presence bits per region
     uint64_t device_bytes() const {
-        return region_slot.bytes + vcs_mask.bytes + vcs_vals.bytes + ht_meta.bytes + ht_slots.bytes + vcs_cbits.bytes;
+        return region_slot.bytes + vcs_mask.bytes + vcs_vals.bytes + ht_meta.bytes + ht_slots.bytes + vcs_cbits.bytes +
+               ht_filter.bytes;
     }
 };
 
@@ -160,7 +162,8 @@ struct DeviceGuard {
 
 void free_scene(vr_scene* s) {
     if (!s) return;
-    DevBuf* bufs[] = {&s->region_slot, &s->vcs_mask, &s->vcs_vals, &s->ht_meta, &s->ht_slots, &s->vcs_cbits};
+    DevBuf* bufs[] = {&s->region_slot, &s->vcs_mask, &s->vcs_vals, &s->ht_meta, &s->ht_slots, &s->vcs_cbits,
+                      &s->ht_filter};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     delete s;
@@ -243,8 +246,9 @@ int build_scene_host(int device, vr_store store, const int32_t* xyz, const uint3
         }
     const uint32_t nr = (uint32_t)region_begin.size();
     region_begin.push_back(m);
-    if (store == VR_STORE_VCS && nr > vr::kVcsMaxRegions)
-        return fail(VR_E_INVALID, "VCS scene with " + std::to_string(nr) + " occupied 64^3 regions (at most " +
+    if (nr > vr::kVcsMaxRegions)
+        return fail(VR_E_INVALID, std::string(store == VR_STORE_VCS ? "VCS" : "hashtable") + " scene with " +
+                                      std::to_string(nr) + " occupied 64^3 regions (at most " +
                                       std::to_string(vr::kVcsMaxRegions) + ")");
 
     vr_scene* s = new vr_scene();
@@ -380,10 +384,31 @@ int build_scene_device(int device, vr_store store, const int32_t* xyz, const uin
     return VR_OK;
 }
 
+// The derived per-region key-presence bits of a cuckoo scene (vr_internal.h KScene::ht_filter),
+// made on the device from the tables either builder wrote.
+int add_hash_filter(vr_scene* s, hipStream_t stream) {
+    DeviceGuard dg(s->device);
+    const uint32_t nr = std::max(1u, s->n_regions);
+    const size_t bytes = (size_t)nr * vr::kHashFilterWords * sizeof(uint32_t);
+    hipError_t e = hipMalloc(&s->ht_filter.p, bytes);
+    if (e != hipSuccess) {
+        s->ht_filter.p = nullptr;
+        return hip_fail(e, "hipMalloc(hash filter)");
+    }
+    s->ht_filter.bytes = bytes;
+    e = hipMemsetAsync(s->ht_filter.p, 0, bytes, stream);
+    if (e == hipSuccess && s->n_regions)
+        e = vr::launch_hash_filter((const uint4*)s->ht_meta.p, (const uint2*)s->ht_slots.p, s->n_regions,
+                                   (uint32_t*)s->ht_filter.p, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hip_fail(e, "hash filter");
+    return VR_OK;
+}
+
 // The derived per-region cluster-existence bits of a VCS scene (vr_internal.h KScene),
 // made on the device from the mask records either builder wrote.
 int add_cluster_bits(vr_scene* s, hipStream_t stream) {
-    if (s->store != VR_STORE_VCS) return VR_OK;
+    if (s->store != VR_STORE_VCS) return add_hash_filter(s, stream);
     DeviceGuard dg(s->device);
     const uint32_t nr = std::max(1u, s->n_regions);
     const size_t bytes = (size_t)nr * 16u * sizeof(uint32_t);
@@ -451,6 +476,7 @@ vr::KScene kscene(const vr_scene* s) {
     k.vcs_cbits = (const uint32_t*)s->vcs_cbits.p;
     k.ht_meta = (const uint4*)s->ht_meta.p;
     k.ht_slots = (const uint2*)s->ht_slots.p;
+    k.ht_filter = (const uint32_t*)s->ht_filter.p;
     k.D = s->D;
     k.min_coord = s->min_coord;
     k.n_regions = s->n_regions;

@@ -33,8 +33,12 @@ constexpr uint32_t kCrawlBudget = 1u << 30;
 constexpr uint32_t kDeferMarker = 0xFFFFFFFFu;
 // VCS walks address a region's cluster masks as a 32-bit byte offset from the
 // scene's mask array (64 KB per occupied 64^3 region): at most 65536 occupied
-// regions (4 GB of masks) per VCS scene; the builders reject larger scenes.
+// regions (4 GB of masks) per VCS scene; the builders reject larger scenes.  The
+// same bound holds for cuckoo scenes, whose key-presence filter is 32 KB per
+// occupied region (2 GB at the bound, addressed the same way).
 constexpr uint32_t kVcsMaxRegions = 65536u;
+// words of a cuckoo region's key-presence filter (64^3 bits)
+constexpr uint32_t kHashFilterWords = 8192u;
 
 // Device view of one immutable scene.  All offsets are 32-bit word indices.
 //  region_slot[D^3]          : region index r, or kNone (null StorageStructure*)
@@ -55,6 +59,12 @@ constexpr uint32_t kVcsMaxRegions = 65536u;
 //  VCS   : vcs_cbits[r*16 + w]: bit b set <=> cluster slot 32w+b of region r is present
 //                              (derived from vcs_mask after either build; the crawl
 //                              pass caches a region's 64 B in LDS)
+//  Cuckoo: ht_filter[r*8192 + w]: key-presence bits of region r's tables, one bit per voxel
+//                              of the 64^3 region in the VCS mask-word order: voxel (x,y,z)
+//                              is word vcs_word_index(x,y,z), bit (y&3)<<3 | z&7 (derived
+//                              from ht_slots after either build).  A probe whose key is not
+//                              in the tables -- most of them -- is answered here; the
+//                              tables are probed for the keys they hold.
 struct KScene {
     const uint32_t* region_slot;
     const uint2* vcs_mask;
@@ -62,6 +72,7 @@ struct KScene {
     const uint32_t* vcs_cbits;
     const uint4* ht_meta;
     const uint2* ht_slots;
+    const uint32_t* ht_filter;
     uint32_t D;
     int32_t min_coord;
     uint32_t n_regions;
@@ -148,6 +159,9 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
 uint32_t crawl_grid(uint32_t records, uint32_t rpw);
 // vcs_cbits of a VCS scene from its mask records (one thread per 32 cluster slots).
 hipError_t launch_cluster_bits(const uint2* vcs_mask, uint32_t n_regions, uint32_t* cbits, hipStream_t stream);
+// ht_filter of a cuckoo scene from its tables (one workgroup per region).
+hipError_t launch_hash_filter(const uint4* ht_meta, const uint2* ht_slots, uint32_t n_regions, uint32_t* filter,
+                              hipStream_t stream);
 hipError_t launch_pack_rgb8(const uint32_t* words, uint8_t* rgb, uint64_t n, hipStream_t stream);
 // The 2-D tile deal's layout (vr_render_opts.tile_cols) for rank 0's reassembly: the frame
 // W x H, bands of band_rows rows, column blocks of tile_cols, R ranks dealt with `stride`;

@@ -703,18 +703,19 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             col = s.vcs_vals[vi];
         } else {
             // Cuckoo store (doesVoxelSpaceExist is always true: no cluster skips).
-            // The region's table header is read once per walk, the two slot
-            // indices use a hoisted reciprocal for `% M`, and the step of an
-            // iteration does not depend on its lookup: both slot loads are in
-            // flight while the next position is computed, and a straight-line
-            // body ends in one exit test, as in the VCS walk above.
+            // Every iteration looks its voxel's key up (CuckooHashTable::lookupVoxel,
+            // CuckooHashTable.cuh:59-76).  A key that is not in the tables -- nearly every
+            // probe of a walk -- costs the reference key1 and key2 (8 B) and misses: that is
+            // answered by the region's key-presence filter (KScene::ht_filter, one bit per
+            // voxel, the VCS mask-word order: a wave's neighbouring rays read neighbouring
+            // words), so the loop is one coalesced 4-B load, the voxel step and one exit test.
+            // The key that IS present ends the walk: after the loop its two slots are probed
+            // as the reference does (key1, val1 on a match, else key2, val2), and the bytes
+            // of the table it was found in are counted.  (Round 4 probed both slots of every
+            // iteration -- random HBM reads, 2.3x the algorithmic bytes at C4, L2 hit 0.55.)
             o = add(o, f3{0.0f, 0.0f, 0.0f});      // -0 -> +0 (in_region_bits_nz below)
             if (!this->in_region_bits_nz(o)) return false;
             if (aborted || this->iters >= kBudget) { aborted = true; return false; }
-            const uint4 m = s.ht_meta[reg];        // {base, M, prime, offset}
-            const FastMod fmod = fastmod_setup(m.y);
-            const uint2* t1 = s.ht_slots + m.x;
-            const uint2* t2 = t1 + m.y;
             const Rcp rx = rcp_setup(EQ ? fabsf(d.x) : d.x), ry = rcp_setup(d.y), rz = rcp_setup(d.z);
             const float gx = px ? 1.0f : -1.0f, gy = py ? 1.0f : -1.0f, gz = pz ? 1.0f : -1.0f;
             const float ex = gx * kEps, ey = gy * kEps, ez = gz * kEps;
@@ -723,15 +724,16 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             // no cluster skips here: with every lane's direction in div_fast's domain no
             // numerator (a voxel plane's, >= ~EPSILON/2 from o) leaves it -- no check at all
             const bool okw = __builtin_amdgcn_ballot_w64(!walk_ok) == 0;
-            uint32_t key = 0;
-            uint2 e1{0u, 0u}, e2{0u, 0u};
+            // the region's filter words as a 32-bit byte offset from the scene's (SGPR-base loads)
+            const uint32_t foff = reg << 15;
+            uint32_t fw = 0, bit = 0;
             uint32_t ic = this->iters + (0x42800000u - kBudget);   // biased count (see the VCS walk)
             for (;;) {
-                const uint32_t vx = (uint32_t)f2i(o.x), vy = (uint32_t)f2i(o.y), vz = (uint32_t)f2i(o.z);
-                key = lshl_or(lshl_or(vx, 10u, vy), 10u, vz);              // generate3DPoint (x<<20|y<<10|z)
-                e1 = t1[fastmod(hash1(key, m.w), fmod)];
-                e2 = t2[fastmod(hash2(key, m.z), fmod)];
-                // rayMarchVoxelGrid's voxel step (Renderer.cuh:318-331), while the slots load
+                const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
+                const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
+                fw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s.ht_filter) + (foff | (wi << 2)));
+                __builtin_amdgcn_sched_barrier(0);   // issue the load before the step
+                // rayMarchVoxelGrid's voxel step (Renderer.cuh:318-331), while the word loads
                 const float ax = next_plane_fma(o.x, gx, ex) - o.x, ay = next_plane_fma(o.y, gy, ey) - o.y,
                             az = next_plane_fma(o.z, gz, ez) - o.z;
                 float sMin, sX = 0.0f, sY = 0.0f, sZ = 0.0f;
@@ -754,11 +756,11 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                     }
                     sMin = fminf(sX, fminf(sY, sZ));
                 }
-                // CuckooHashTable::lookupVoxel (CuckooHashTable.cuh:59-76): key1 (+val1 on a
-                // match), else key2 (+val2 on a match)
-                const bool m1 = e1.x == key, m2 = e2.x == key;
-                this->count(m1 ? 8u : (m2 ? 12u : 8u));
-                const uint32_t fm = (m1 | m2) ? ~0u : 0u;
+                // key1 + key2 of a key the tables do not hold; the hit's own bytes are
+                // settled after the loop (8 or 12)
+                this->count(8u);
+                bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
+                const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)fw, bit, 1u);   // 0 or ~0: present
                 if (!SHADOW && !EQ) {                     // a non-hit step: its t values feed the normal
                     tX = fm ? tX : sX; tY = fm ? tY : sY; tZ = fm ? tZ : sZ;
                 }
@@ -771,12 +773,19 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             }
             this->iters = ic - (0x42800000u - kBudget);
             // why the lane left (see the VCS walk): recomputed from VGPR values
-            asm("" : "+v"(e1.x), "+v"(e1.y), "+v"(e2.x), "+v"(e2.y), "+v"(key), "+v"(o.x), "+v"(o.y), "+v"(o.z));
-            const bool m1 = e1.x == key, found = m1 || e2.x == key;
-            if (!found) {
+            asm("" : "+v"(fw), "+v"(bit), "+v"(o.x), "+v"(o.y), "+v"(o.z));
+            if (!__builtin_amdgcn_ubfe(fw, bit, 1u)) {
                 if (this->in_region_bits_nz(o)) aborted = true;    // budget spent inside the region
                 return false;
             }
+            // the hit (o unstepped: the probed voxel): CuckooHashTable::lookupVoxel's two probes
+            const uint32_t key = lshl_or(lshl_or((uint32_t)f2i(o.x), 10u, (uint32_t)f2i(o.y)), 10u, (uint32_t)f2i(o.z));
+            const uint4 m = s.ht_meta[reg];        // {base, M, prime, offset}
+            const uint2* t1 = s.ht_slots + m.x;
+            const uint2 e1 = t1[hash1(key, m.w) % m.y];
+            const uint2 e2 = t1[m.y + hash2(key, m.z) % m.y];
+            const bool m1 = e1.x == key;
+            this->count(m1 ? 0u : 4u);             // key1 + val1 (8, counted above), or key1 + key2 + val2
             col = m1 ? e1.y : e2.y;
         }
         if (col == kEmpty) return false;
@@ -1806,6 +1815,21 @@ __global__ void cluster_bits_kernel(const uint2* __restrict__ mask, uint32_t n_r
     cbits[t] = b;
 }
 
+// KScene::ht_filter: workgroup r sets the presence bit of every key in region r's two tables
+// (keys are local generate3DPoint keys: x, y, z < 64)
+__global__ void hash_filter_kernel(const uint4* __restrict__ meta, const uint2* __restrict__ slots,
+                                   uint32_t* __restrict__ filter) {
+    using F = Ctx<STORE_VCS, false, kTileBudget>;
+    const uint4 m = meta[blockIdx.x];
+    uint32_t* f = filter + (size_t)blockIdx.x * kHashFilterWords;
+    for (uint32_t i = threadIdx.x; i < 2u * m.y; i += blockDim.x) {
+        const uint32_t k = slots[m.x + i].x;
+        if (k == kEmpty) continue;
+        const uint32_t x = (k >> 20) & 63u, y = (k >> 10) & 63u, z = k & 63u;
+        atomicOr(&f[F::word_index(x, y, z)], 1u << (F::word_bit5(y, z) & 31u));
+    }
+}
+
 __global__ void pack_rgb8_kernel(const uint32_t* __restrict__ w, uint8_t* __restrict__ rgb, uint64_t n) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1934,6 +1958,13 @@ hipError_t launch_assemble_tiles(const void* parts, void* frame, uint32_t elem_b
     case 3: hipLaunchKernelGGL(assemble_tiles_kernel<3>, grid, block, 0, stream, p, f, t); break;
     default: hipLaunchKernelGGL(assemble_tiles_kernel<4>, grid, block, 0, stream, p, f, t); break;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_hash_filter(const uint4* ht_meta, const uint2* ht_slots, uint32_t n_regions, uint32_t* filter,
+                              hipStream_t stream) {
+    if (n_regions == 0) return hipSuccess;
+    hipLaunchKernelGGL(hash_filter_kernel, dim3(n_regions), dim3(256), 0, stream, ht_meta, ht_slots, filter);
     return hipGetLastError();
 }
 
