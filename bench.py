@@ -410,7 +410,11 @@ def main():
             hbm = traffic / (kern_ms * 1e-3) / 1e9
             hbm_frac = hbm / HBM_PEAK_GBS
             roof.update({"hbm_measured_gbs": round(hbm, 1), "hbm_measured_frac": round(hbm_frac, 4),
-                         "algorithmic_over_hbm_bytes": round(launch_bytes / traffic, 1)})
+                         "algorithmic_over_hbm_bytes": round(launch_bytes / traffic, 1),
+                         "traffic_kernel": tj.get("kernel"),
+                         "traffic_basis": "PMC (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction) of ONE launch alone of "
+                                          "the tile-pass kernel named in traffic_kernel (the lone-frame occupancy "
+                                          "variant), profiles/traffic.json"})
         if tj.get("valu_insts_per_launch") and tj.get("grbm_gui_active_per_launch") and tj.get("rocprof_avg_ns"):
             # VALU issue of the dependent walk: 2 cycles per wave64 instruction on each of the
             # 1024 SIMD-32s, at the clock the profile measured (GRBM_GUI_ACTIVE sums the 8 XCDs)
@@ -424,6 +428,9 @@ def main():
             roof["profile_clock_ghz"] = round(ghz, 3)
             if tj.get("lane_util") is not None:
                 roof["valu_lane_utilisation"] = tj["lane_util"]
+                # the share of the chip's VALU lane-slots doing a lane's work: issue x lane utilisation
+                roof["valu_useful_frac"] = round(valu_frac * tj["lane_util"], 4)
+                roof["valu_useful_frac_pipelined"] = round(roof["valu_issue_frac_pipelined"] * tj["lane_util"], 4)
         if hbm_frac is not None and valu_frac is not None:
             roof["bound"] = "valu" if valu_frac >= hbm_frac else "hbm"
             roof["bound_basis"] = ("the measured limiter: VALU issue fraction vs measured HBM fraction "

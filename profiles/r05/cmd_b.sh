@@ -7,11 +7,11 @@ O=${1:-gpurun_out/r05b}
 mkdir -p $O
 export TMPDIR=/tmp
 for R in 1 0; do
-  timeout -s KILL 300 rocprofv3 --kernel-trace -d $O/tr_r$R -o run -- python3 profiles/r05/rank_trace.py --rank $R > $O/tr_r$R.log 2>&1 || { tail -5 $O/tr_r$R.log; exit 1; }
+  timeout -s KILL 300 rocprofv3 --kernel-trace -f csv -d $O/tr_r$R -o run -- python3 profiles/r05/rank_trace.py --rank $R > $O/tr_r$R.log 2>&1 || { tail -5 $O/tr_r$R.log; exit 1; }
   python3 profiles/r05/rank_trace_split.py $(ls $O/tr_r$R/*kernel_trace.csv | head -1) > $O/split_r$R.txt || exit 1
   echo "rank $R of 8:"; cat $O/split_r$R.txt
 done
-timeout -s KILL 300 rocprofv3 --kernel-trace -d $O/tr_w1 -o run -- python3 profiles/r05/rank_trace.py --world 1 --rank 0 --steps 40 --lone 10 > $O/tr_w1.log 2>&1 || { tail -5 $O/tr_w1.log; exit 1; }
+timeout -s KILL 300 rocprofv3 --kernel-trace -f csv -d $O/tr_w1 -o run -- python3 profiles/r05/rank_trace.py --world 1 --rank 0 --steps 40 --lone 10 > $O/tr_w1.log 2>&1 || { tail -5 $O/tr_w1.log; exit 1; }
 python3 profiles/r05/rank_trace_split.py $(ls $O/tr_w1/*kernel_trace.csv | head -1) 40 20 10 > $O/split_w1.txt || exit 1
 echo "one GPU:"; cat $O/split_w1.txt
 VR_CRAWL_RPW=1 timeout -k 10 500 python profiles/rank_projection.py --config C5 --world 8 > $O/proj_rpw1.jsonl 2> $O/proj_rpw1.err || { tail -5 $O/proj_rpw1.err; exit 1; }
