@@ -7,7 +7,7 @@ import sys
 
 path = sys.argv[1]
 steps, warm, lone = (int(x) for x in sys.argv[2:5]) if len(sys.argv) > 4 else (100, 20, 30)
-rows = [r for r in csv.DictReader(open(path)) if "vr::" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(path)) if any(k in r["Kernel_Name"] for k in ("march_kernel", "crawl_kernel", "pack_rgb8"))]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows]
 per = 3
