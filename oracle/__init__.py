@@ -84,6 +84,8 @@ def lib() -> ctypes.CDLL:
         L.or_pixel_stats.restype = c_int
         L.or_set_iter_budget.argtypes = [c_uint64]
         L.or_set_iter_budget.restype = None
+        L.or_cycle_selftest.argtypes = [c_uint32, c_uint32, c_uint32]
+        L.or_cycle_selftest.restype = ctypes.c_int64
         _lib = L
     return _lib
 

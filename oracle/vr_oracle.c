@@ -392,6 +392,20 @@ static inline int cycle_step(cycle* y, v3i c, v3f o) {
     return 0;
 }
 
+/* Test hook for the cycle test alone: a loop whose state sequence is `prefix` distinct
+ * states, then `period` distinct states repeating (period 0: never repeats).  Returns the
+ * round at which cycle_step reports the repeat, or -1 if none within max_rounds. */
+int64_t or_cycle_selftest(uint32_t prefix, uint32_t period, uint32_t max_rounds) {
+    #define OR_STATE(k) ((v3i){{(int32_t)(k), -(int32_t)(k), 7}}), V3((float)(k) * 0.5f, 1.0f, (float)(k))
+    cycle y = cycle_start(OR_STATE(0u));
+    for (uint32_t r = 1; r <= max_rounds; ++r) {
+        const uint32_t k = (period == 0u || r < prefix) ? r : prefix + (r - prefix) % period;
+        if (cycle_step(&y, OR_STATE(k))) return (int64_t)r;
+    }
+    #undef OR_STATE
+    return -1;
+}
+
 /* VoxelScene::isRayInScene (Renderer.cuh:38-44) */
 static inline int in_scene(const ctx* c, v3i r) {
     uint32_t D = c->s->D, mc = (uint32_t)c->s->min_coord;

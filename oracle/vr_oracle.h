@@ -81,6 +81,10 @@ int or_scene_cuckoo_table(const or_scene* s, uint32_t r, uint32_t key, int* reha
  * (process-global; UINT64_MAX = none, the default).  A pixel that exceeds it
  * renders as 0 with 4 bytes, like a walk that never finishes. */
 void or_set_iter_budget(uint64_t budget);
+/* Test hook: the region-level loops' cycle test (Brent) on a synthetic state sequence --
+ * `prefix` distinct states, then `period` distinct states repeating (0: none); the round
+ * the repeat is found at, or -1. */
+int64_t or_cycle_selftest(uint32_t prefix, uint32_t period, uint32_t max_rounds);
 
 /* Known-answer helpers. */
 int32_t or_hash1(int32_t key, uint32_t offset);                 /* CuckooHashTable.cuh:181-190 */

@@ -56,3 +56,53 @@ def test_launches_in_flight_on_three_streams(c5_scene, kernel, algo):
     vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, last, r0, r1, kernel=kernel)
     torch.cuda.synchronize()
     assert torch.equal(last, ref)
+
+
+def test_render_refuses_graph_capture(c5_scene):
+    """vr_render* on a stream that is capturing a graph returns VR_E_INVALID before enqueuing
+    anything (include/vr.h): the slot ring's event wait/record and the work order's host-side
+    bookkeeping would be baked into the graph and not replay.  The capture itself stays
+    usable: it ends cleanly, and a render after it is exact."""
+    cfg, scene = c5_scene
+    W, H = 64, 48
+    cam, lit = vr.Camera.reference(W, H), vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    ref = vr.run_raymarching_kernel(scene, vr.RayMarchAlgorithm.ORIGINAL, cam, lit, info, W, H).clone()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    err = None
+    with torch.cuda.graph(g, stream=s):
+        try:
+            vr.render_ex(scene, vr.RayMarchAlgorithm.ORIGINAL, cam, lit, info, W, H, out, stream=s)
+        except vr.VrError as e:
+            err = e
+    assert err is not None and err.code == -1 and "captur" in str(err)
+    torch.cuda.synchronize()
+    vr.render_ex(scene, vr.RayMarchAlgorithm.ORIGINAL, cam, lit, info, W, H, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
+def test_crawl_stats_credit_unloaded_reads(c5_scene):
+    """vr_render_opts.stats_dev: [0] crawl iterations fast-forwarded in closed form, [1] the
+    existence-read bytes credited without a load -- 4 per fast-forwarded iteration plus 4 per
+    crawl-pass skip step answered from the LDS cluster bits (round 5) -- a part of the
+    counted bytes.  C5's crawl rows have both; a frame that defers nothing has neither."""
+    cfg, scene = c5_scene
+    W, H = cfg.width, cfg.height
+    cam, lit = vr.Camera.reference(W, H), vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    out = torch.empty(16 * W, dtype=torch.int32, device="cuda")
+    ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+    st = torch.zeros(2, dtype=torch.int64, device="cuda")
+    vr.render_ex(scene, vr.RayMarchAlgorithm.ORIGINAL, cam, lit, info, W, H, out, 696, 712, counter=ctr, stats=st)
+    torch.cuda.synchronize()
+    n, b, total = int(st[0]), int(st[1]), int(ctr.item())
+    assert n > 1_000_000 and b > 4 * n and b < total, (n, b, total)
+    ctr.zero_()
+    st.zero_()
+    vr.render_ex(scene, vr.RayMarchAlgorithm.ORIGINAL, cam, lit, info, W, H, out, 0, 16, counter=ctr, stats=st)
+    torch.cuda.synchronize()
+    assert int(st[0]) == 0 and int(st[1]) == 0 and int(ctr.item()) > 0

@@ -420,3 +420,20 @@ def test_fuzz_cases_python_restatement(seed):
         for algo in (oracle.ALGO_ORIGINAL, oracle.ALGO_LONGESTAXIS):
             _rays_agree(sc, ps, algo, cam, lit, plit, c.W, c.H, c.scale, px, py, translation=c.translation,
                         where=(seed, store))
+
+
+def test_cycle_detection_finds_every_period():
+    """The region-level loops' never-finishes test (Brent's cycle detection, oracle
+    cycle_step = the kernels' Ctx::cycle_step, DESIGN.md 2): a state sequence that
+    repeats with any prefix and period is found within about twice (prefix + period)
+    rounds -- round 4 compared each round with the one before only (period 1) -- and a
+    sequence that never repeats is never reported."""
+    L = oracle.lib()
+    for prefix in range(0, 40, 3):
+        for period in range(1, 40, 2):
+            r = L.or_cycle_selftest(prefix, period, 100000)
+            assert r > 0, (prefix, period)
+            assert r >= max(prefix, 1) + period - 1, (prefix, period, r)   # not before a repeat exists
+            assert r <= 2 * (prefix + period) + period + 2, (prefix, period, r)
+    assert L.or_cycle_selftest(0, 1, 10) == 1                               # a fixed point: at once
+    assert L.or_cycle_selftest(5, 0, 200000) == -1

@@ -673,6 +673,22 @@ bool in_flight_occupancy() {
     }();
     return on;
 }
+// (A/B, round 5) VR_PRIO_HEAD_DIV=d: the first n/d workgroups of a heaviest-first order run at
+// raised issue priority; VR_PRIO_ESC=t: waves whose primary walks exceed t iterations raise
+// theirs for the shadow walks.  Off by default.
+uint32_t env_u32(const char* name) {
+    const char* e = std::getenv(name);
+    const long v = e ? std::strtol(e, nullptr, 10) : 0;
+    return (uint32_t)(v > 0 ? v : 0);
+}
+uint32_t prio_head_div() {
+    static const uint32_t r = env_u32("VR_PRIO_HEAD_DIV");
+    return r;
+}
+uint32_t prio_esc() {
+    static const uint32_t r = env_u32("VR_PRIO_ESC");
+    return r;
+}
 bool order_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("VR_ORDER");
@@ -755,6 +771,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         }
         const bool match = O.valid && O.gx == gx && O.gy == gy;
         v.order = match ? O.order : nullptr;
+        v.prio_head = (match && prio_head_div()) ? n / prio_head_div() : 0u;
         remake = !match || ++O.age >= order_refresh();
         v.cost = remake ? O.cost : nullptr;
     }
@@ -762,6 +779,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // the same pixels)
     const vr::KScene ks = kscene(s);
     const uint32_t cwgs = vr::crawl_grid(expect, v.crawl_rpw);
+    v.prio_esc = prio_esc();
     // the tile pass's occupancy variant (vr_occupancy): AUTO = the in-flight one while another
     // stream's launch is running
     const bool hi = occupancy == VR_OCCUPANCY_IN_FLIGHT ||

@@ -129,6 +129,10 @@ struct KView {
     // loop iterations) to cost[tile * kWavesPerTileGroup + wave], tile = row * columns + column.
     const uint32_t* order;
     uint32_t* cost;
+    // (A/B, round 5) issue priority of heavy waves: the first prio_head workgroups of a
+    // heaviest-first order run at s_setprio 3; prio_esc > 0: a wave whose primary walks took
+    // more than prio_esc iterations raises its priority to 2 for its shadow walks
+    uint32_t prio_head, prio_esc;
 };
 
 // Rays that start a cluster-skip crawl (see vr_march.hip crawl_steps) in the

@@ -1534,7 +1534,13 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
         Walker<STORE, COUNT, CRAWL> w(s, v);
         attach(w, cl);
         Hit h;
-        if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
+        const bool hit = w.template primary<ALGO>(ro, rd, h);
+        if (!CRAWL && v.prio_esc) {
+            uint32_t m = w.iters;
+            for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+            if (m > v.prio_esc) __builtin_amdgcn_s_setprio(2);
+        }
+        if (hit) col = light_and_shadow(w, v, h);
         if (iters) *iters = w.iters;              // the walk's length (the work order's cost)
         bytes = w.bytes + 4u;                     // + the pixel write
         if (ff) *ff = uint2{w.ff, w.nl};
@@ -1640,6 +1646,7 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, (TileWaves<ALGO, HI>::value
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t bx, by;
     tile_group(v, bx, by);
+    if (v.order && blockIdx.y * gridDim.x + blockIdx.x < v.prio_head) __builtin_amdgcn_s_setprio(3);
     const uint32_t x = (bx * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
     const uint32_t l = (by * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
     uint32_t bytes = 0, iters = 0;
