@@ -231,20 +231,10 @@ typedef struct {
      * (long walks are spatially clustered) are spread over all ranks. */
     uint32_t tile_cols;
     uint32_t deal_stride;
-    /* (round 5) vr_sparse: how the VCS original walk's tile pass tests a cluster's existence.
-     * Pixels and counted bytes never depend on it. */
-    uint32_t sparse;
+    uint32_t reserved2;   /* 0 */
 } vr_render_opts;
 /* The smallest struct_size accepted: the layout up to and including `reserved`. */
 #define VR_RENDER_OPTS_MIN_SIZE 48u
-
-/* OFF: one 8-B mask-word load per iteration answers existence and presence (the dense walk:
- * the words mostly hit the vector L1).  ON: the region's 64-B cluster-existence bits are read
- * first and the mask word only in a present cluster, so a skip through an absent cluster waits
- * for an L1/L2 hit instead of a mask record's line from MALL/HBM (sparse scenes, whose walks
- * are mostly such skips).  AUTO: ON for a scene whose occupied regions hold fewer than 1 in 8
- * of their cluster slots (C5: 1 in 20, C2: 3 in 10). */
-typedef enum { VR_SPARSE_AUTO = 0, VR_SPARSE_OFF = 1, VR_SPARSE_ON = 2 } vr_sparse;
 
 typedef enum {
     VR_OCCUPANCY_AUTO = 0,

@@ -30,8 +30,7 @@ def oracle_lighting_from(lit) -> "oracle.OrLighting":
     return o
 
 
-def gpu_render(scene, algo, cam, lit, info, W, H, row_begin=0, row_end=None, count=False, kernel=None, defer_cap=0,
-               sparse=None):
+def gpu_render(scene, algo, cam, lit, info, W, H, row_begin=0, row_end=None, count=False, kernel=None, defer_cap=0):
     import torch
 
     import voxelraymarcher_amd as vr
@@ -39,10 +38,10 @@ def gpu_render(scene, algo, cam, lit, info, W, H, row_begin=0, row_end=None, cou
     kernel = vr.Kernel.AUTO if kernel is None else kernel
     out = torch.full(((row_end - row_begin) * W,), -1, dtype=torch.int32, device="cuda")
     nbytes = None
-    if count or defer_cap or sparse is not None:
+    if count or defer_cap:
         ctr = torch.zeros(1, dtype=torch.int64, device="cuda") if count else None
         vr.render_ex(scene, algo, cam, lit, info, W, H, out, row_begin, row_end, counter=ctr, kernel=kernel,
-                     defer_cap=defer_cap, sparse=vr.Sparse.AUTO if sparse is None else sparse)
+                     defer_cap=defer_cap)
         torch.cuda.synchronize()
         nbytes = int(ctr.item()) if count else None
     else:

@@ -45,7 +45,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_capi.VrLighting) == 44
     assert ctypes.sizeof(_capi.VrRenderOpts) == 72          # round 5: + occupancy, tile deal
     assert _capi.VrRenderOpts.reserved.offset + 4 == _capi.VR_RENDER_OPTS_MIN_SIZE
-    assert _capi.VrRenderOpts.occupancy.offset == 56 and _capi.VrRenderOpts.sparse.offset == 68
+    assert _capi.VrRenderOpts.occupancy.offset == 56 and _capi.VrRenderOpts.reserved2.offset == 68
     assert ctypes.sizeof(_capi.VrSynthParams) == 40
     assert f"#define VR_RENDER_OPTS_MIN_SIZE {_capi.VR_RENDER_OPTS_MIN_SIZE}u" in open(
         os.path.join(ROOT, "include", "vr.h")).read()
@@ -60,7 +60,7 @@ def test_render_opts_versioning():
     _capi.check(vr.lib().vr_render_opts_init(ctypes.byref(o)), "init")
     assert o.struct_size == ctypes.sizeof(o) and o.nranks == 1 and o.row_end == 0xFFFFFFFF
     assert (o.kernel, o.schedule, o.defer_cap, o.reserved) == (0, 0, 0, 0) and not o.bytes_dev and not o.stats_dev
-    assert (o.occupancy, o.tile_cols, o.deal_stride, o.sparse) == (0, 0, 0, 0)
+    assert (o.occupancy, o.tile_cols, o.deal_stride, o.reserved2) == (0, 0, 0, 0)
 
     class OldOpts(ctypes.Structure):      # the round-3 layout
         _fields_ = [("kernel", ctypes.c_uint32), ("row_begin", ctypes.c_uint32), ("row_end", ctypes.c_uint32),

@@ -50,13 +50,6 @@ def check_frame(xyz, rgb, store, algo, W, H, scale, cam=None, lit=None, translat
             got2, _ = gpu_render(scene, algo, cam, lit, info, W, H, row_begin, row_end, count=False, kernel=kernel,
                                  defer_cap=cap)
             assert np.array_equal(got2, want), f"{tag} (uncounted): " + diff_report(got2, want, W, row_begin)
-            if store == vr.StorageType.VOXEL_CLUSTER_STORE and algo == vr.RayMarchAlgorithm.ORIGINAL:
-                # both existence tests of the VCS original walk (vr_sparse), whatever AUTO picks
-                for sp in (vr.Sparse.ON, vr.Sparse.OFF):
-                    got3, _ = gpu_render(scene, algo, cam, lit, info, W, H, row_begin, row_end, kernel=kernel,
-                                         defer_cap=cap, sparse=sp)
-                    assert np.array_equal(got3, want), f"{tag} sparse={sp.name}: " + diff_report(got3, want, W,
-                                                                                                   row_begin)
     return want
 
 

@@ -51,7 +51,6 @@ class VrSynthParams(ctypes.Structure):
 VR_KERNEL_AUTO, VR_KERNEL_TILE, VR_KERNEL_TILE_REWALK = 0, 1, 3
 VR_SCHEDULE_AUTO, VR_SCHEDULE_GRID, VR_SCHEDULE_HEAVIEST_FIRST = 0, 1, 2
 VR_OCCUPANCY_AUTO, VR_OCCUPANCY_LONE, VR_OCCUPANCY_IN_FLIGHT = 0, 1, 2
-VR_SPARSE_AUTO, VR_SPARSE_OFF, VR_SPARSE_ON = 0, 1, 2
 
 
 class VrRenderOpts(ctypes.Structure):
@@ -59,7 +58,7 @@ class VrRenderOpts(ctypes.Structure):
     _fields_ = [("struct_size", c_uint32), ("kernel", c_uint32), ("row_begin", c_uint32), ("row_end", c_uint32),
                 ("band_rows", c_uint32), ("rank", c_uint32), ("nranks", c_uint32), ("defer_cap", c_uint32),
                 ("bytes_dev", c_void_p), ("schedule", c_uint32), ("reserved", c_uint32), ("stats_dev", c_void_p),
-                ("occupancy", c_uint32), ("tile_cols", c_uint32), ("deal_stride", c_uint32), ("sparse", c_uint32)]
+                ("occupancy", c_uint32), ("tile_cols", c_uint32), ("deal_stride", c_uint32), ("reserved2", c_uint32)]
 
 
 VR_RENDER_OPTS_MIN_SIZE = 48
@@ -145,7 +144,6 @@ def f3(v) -> ctypes.Array:
 __all__ = ["lib", "check", "VrCamera", "VrLighting", "VrRenderOpts", "VR_RENDER_OPTS_MIN_SIZE", "VR_KERNEL_AUTO",
            "VR_KERNEL_TILE", "VR_KERNEL_TILE_REWALK", "VR_SCHEDULE_AUTO", "VR_SCHEDULE_GRID",
            "VR_SCHEDULE_HEAVIEST_FIRST", "VR_OCCUPANCY_AUTO", "VR_OCCUPANCY_LONE", "VR_OCCUPANCY_IN_FLIGHT",
-           "VR_SPARSE_AUTO", "VR_SPARSE_OFF", "VR_SPARSE_ON",
            "VrSceneInfo", "VrSynthParams", "VrError", "SIGNATURES",
            "VR_STORE_VCS", "VR_STORE_HASHTABLE", "VR_ALGO_LONGESTAXIS", "VR_ALGO_ORIGINAL", "f3", "LIB_PATH",
            "c_uint8"]

@@ -136,7 +136,6 @@ struct vr_scene {
     uint32_t D = 1;
     int32_t min_coord = 0;
     uint32_t n_regions = 0;
-    uint64_t n_clusters = 0;   // VCS: present 8^3 clusters (popcount of vcs_cbits), for vr_sparse AUTO
     uint64_t n_voxels = 0;
     DevBuf region_slot, vcs_mask, vcs_vals, ht_meta, ht_slots;
     DevBuf vcs_cbits;   // derived (not part of vr_scene_digest): cluster-existence bits per region
@@ -424,13 +423,6 @@ int add_cluster_bits(vr_scene* s, hipStream_t stream) {
         e = vr::launch_cluster_bits((const uint2*)s->vcs_mask.p, s->n_regions, (uint32_t*)s->vcs_cbits.p, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hip_fail(e, "cluster bits");
-    // the scene's cluster occupancy (vr_sparse AUTO): the bits, popcounted on the host
-    std::vector<uint32_t> bits((size_t)nr * 16u);
-    e = hipMemcpy(bits.data(), s->vcs_cbits.p, bytes, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return hip_fail(e, "cluster bits D2H");
-    uint64_t c = 0;
-    for (uint32_t w : bits) c += (uint64_t)__builtin_popcount(w);
-    s->n_clusters = s->n_regions ? c : 0;
     return VR_OK;
 }
 
@@ -681,30 +673,6 @@ bool in_flight_occupancy() {
     }();
     return on;
 }
-// (A/B, round 5) VR_PRIO_HEAD_DIV=d: the first n/d workgroups of a heaviest-first order run at
-// raised issue priority; VR_PRIO_ESC=t: waves whose primary walks exceed t iterations raise
-// theirs for the shadow walks.  Off by default.
-uint32_t env_u32(const char* name) {
-    const char* e = std::getenv(name);
-    const long v = e ? std::strtol(e, nullptr, 10) : 0;
-    return (uint32_t)(v > 0 ? v : 0);
-}
-uint32_t prio_head_div() {
-    static const uint32_t r = env_u32("VR_PRIO_HEAD_DIV");
-    return r;
-}
-uint32_t prio_esc() {
-    static const uint32_t r = env_u32("VR_PRIO_ESC");
-    return r;
-}
-// VR_SPARSE=0 / 1 (A/B runs): what VR_SPARSE_AUTO means for every launch (OFF / ON)
-int sparse_env() {
-    static const int r = [] {
-        const char* e = std::getenv("VR_SPARSE");
-        return e ? (e[0] == '1' ? 1 : (e[0] == '0' ? 0 : -1)) : -1;
-    }();
-    return r;
-}
 bool order_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("VR_ORDER");
@@ -713,17 +681,12 @@ bool order_enabled() {
     return on;
 }
 
-// vr_sparse AUTO: a VCS scene whose occupied regions hold fewer than 1 in 8 of their cluster
-// slots (C5: 1 in 20; C2: 3 in 10)
-constexpr uint64_t kSparseClusterDiv = 8;
-
-int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, uint32_t occupancy, uint32_t sparse,
-           vr::KView& v, void* stream) {
+int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, uint32_t occupancy, vr::KView& v,
+           void* stream) {
     if (algo != VR_ALGO_ORIGINAL && algo != VR_ALGO_LONGESTAXIS) return fail(VR_E_INVALID, "unknown algorithm");
     if (kernel != VR_KERNEL_AUTO && kernel != VR_KERNEL_TILE && kernel != VR_KERNEL_TILE_REWALK)
         return fail(VR_E_INVALID, "unknown kernel (2, the persistent kernel, was retired)");
     if (occupancy > VR_OCCUPANCY_IN_FLIGHT) return fail(VR_E_INVALID, "unknown occupancy");
-    if (sparse > VR_SPARSE_ON) return fail(VR_E_INVALID, "unknown sparse mode");
     if (v.local_rows == 0 || v.LW == 0) return VR_OK;
     DeviceGuard dg(s->device);
     const bool count = v.bytes != nullptr;
@@ -792,7 +755,6 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         }
         const bool match = O.valid && O.gx == gx && O.gy == gy;
         v.order = match ? O.order : nullptr;
-        v.prio_head = (match && prio_head_div()) ? n / prio_head_div() : 0u;
         remake = !match || ++O.age >= order_refresh();
         v.cost = remake ? O.cost : nullptr;
     }
@@ -800,17 +762,11 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // the same pixels)
     const vr::KScene ks = kscene(s);
     const uint32_t cwgs = vr::crawl_grid(expect, v.crawl_rpw);
-    v.prio_esc = prio_esc();
     // the tile pass's occupancy variant (vr_occupancy): AUTO = the in-flight one while another
     // stream's launch is running
     const bool hi = occupancy == VR_OCCUPANCY_IN_FLIGHT ||
                     (occupancy == VR_OCCUPANCY_AUTO && !alone && in_flight_occupancy());
-    // the sparse existence test (vr_sparse): AUTO = fewer than 1 in kSparseClusterFrac of the
-    // occupied regions' cluster slots present
-    const bool auto_sp = sparse_env() >= 0 ? sparse_env() == 1
-                                           : s->n_clusters * kSparseClusterDiv < (uint64_t)s->n_regions * 512u;
-    const bool sp = s->store == VR_STORE_VCS && (sparse == VR_SPARSE_ON || (sparse == VR_SPARSE_AUTO && auto_sp));
-    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs, hi, sp);
+    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs, hi);
     if (e == hipSuccess && remake) {
         // (on a side stream instead -- one more stream than the box's 4 hardware queues
         // serialised the two render streams: C2 0.1124 -> 0.1277 ms per frame in flight,
@@ -1144,6 +1100,7 @@ int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr
     const uint32_t row_end = o.row_end == 0xFFFFFFFFu ? height : o.row_end;
     if (o.row_begin > row_end || row_end > height) return fail(VR_E_INVALID, "bad row range");
     if (!o.nranks || o.rank >= o.nranks) return fail(VR_E_INVALID, "bad band partition");
+    if (o.reserved2 != 0u) return fail(VR_E_INVALID, "vr_render_opts.reserved2 must be 0");
     const uint32_t rows = row_end - o.row_begin;
     const uint32_t band = o.band_rows ? o.band_rows : std::max(1u, rows);
     v.row0 = o.row_begin;
@@ -1174,7 +1131,7 @@ int vr_render_ex(const vr_scene* s, vr_algo algo, const vr_camera* cam, const vr
     v.stats = o.bytes_dev ? (unsigned long long*)o.stats_dev : nullptr;
     v.defer_cap = o.defer_cap;
     if (o.schedule > VR_SCHEDULE_HEAVIEST_FIRST) return fail(VR_E_INVALID, "unknown schedule");
-    return launch(s, algo, o.kernel, o.schedule, o.occupancy, o.sparse, v, stream);
+    return launch(s, algo, o.kernel, o.schedule, o.occupancy, v, stream);
 }
 
 int vr_render_opts_init(vr_render_opts* opts) {

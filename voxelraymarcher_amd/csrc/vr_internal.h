@@ -129,10 +129,6 @@ struct KView {
     // loop iterations) to cost[tile * kWavesPerTileGroup + wave], tile = row * columns + column.
     const uint32_t* order;
     uint32_t* cost;
-    // (A/B, round 5) issue priority of heavy waves: the first prio_head workgroups of a
-    // heaviest-first order run at s_setprio 3; prio_esc > 0: a wave whose primary walks took
-    // more than prio_esc iterations raises its priority to 2 for its shadow walks
-    uint32_t prio_head, prio_esc;
 };
 
 // Rays that start a cluster-skip crawl (see vr_march.hip crawl_steps) in the
@@ -157,10 +153,8 @@ constexpr uint32_t kDeferWords = 4 + kDeferCap * kDeferRecWords;
 // `stream`, the crawl pass with `crawl_wgs` workgroups (any number is correct).
 // in_flight: another stream's launch is still running on the device (the tile pass then
 // takes its higher-occupancy variant where one exists, vr_march.hip TileWaves)
-// sparse: the VCS original walk's tile pass tests cluster existence from vcs_cbits first
-// (vr_sparse; vr_march.hip Walker SPARSE)
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,
-                        hipStream_t stream, uint32_t crawl_wgs, bool in_flight, bool sparse);
+                        hipStream_t stream, uint32_t crawl_wgs, bool in_flight);
 // Crawl-pass grid for a launch that expects about `records` deferred pixels.
 uint32_t crawl_grid(uint32_t records, uint32_t rpw);
 // vcs_cbits of a VCS scene from its mask records (one thread per 32 cluster slots).

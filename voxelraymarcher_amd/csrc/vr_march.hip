@@ -289,11 +289,7 @@ __device__ __forceinline__ void tile_group(const KView& v, uint32_t& bx, uint32_
 // through its walk loop: C4 0.085 -> 0.109 ms per frame, profiles/r03/ab_exact_cuckoo.txt.)
 template <int STORE, bool CRAWL>
 struct ExactWalk { static constexpr bool value = CRAWL; };
-// SPARSE (tile pass, VCS original walk; vr_sparse): the walk's existence test reads the region's
-// cluster-existence bits (KScene::vcs_cbits, 64 B per region: L1/L2-resident) and loads the
-// voxel's mask word only in a present cluster -- a skip through an absent cluster then waits
-// for an L1/L2 hit instead of the 128-B mask record's line from MALL/HBM.
-template <int STORE, bool COUNT, bool CRAWL, bool SPARSE = false>
+template <int STORE, bool COUNT, bool CRAWL>
 struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget : kTileBudget> {
     using C = Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget : kTileBudget>;
     static constexpr bool kExact = ExactWalk<STORE, CRAWL>::value;
@@ -492,14 +488,6 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                                 if (COUNT && !pres) ++this->nl;   // counted above, never loaded
                                 blk = Blk{0u, kNone};
                                 if (pres)
-                                    blk = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) +
-                                                                          (moff | (wi << 3)));
-                            } else if constexpr (SPARSE) {
-                                const uint32_t cw = *reinterpret_cast<const uint32_t*>(
-                                    reinterpret_cast<const char*>(s.vcs_cbits) + ((reg << 6) | ((wi >> 9) << 2)));
-                                const bool pres = (cw >> ((wi >> 4) & 31u)) & 1u;
-                                blk = Blk{0u, kNone};
-                                if (__builtin_amdgcn_ballot_w64(pres) != 0 && pres)
                                     blk = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) +
                                                                           (moff | (wi << 3)));
                             } else {
@@ -1481,8 +1469,8 @@ __device__ __forceinline__ bool pixel_ray(const KView& v, uint32_t x, uint32_t l
 
 // applyLighting at the primary hit (Renderer.cuh:249-258; regionWorldPosition :413)
 // times !shadow (:315,737,821): the pixel's colour.
-template <int STORE, bool COUNT, bool CRAWL, bool SPARSE>
-__device__ __forceinline__ uint32_t light_and_shadow(Walker<STORE, COUNT, CRAWL, SPARSE>& w, const KView& v, const Hit& h) {
+template <int STORE, bool COUNT, bool CRAWL>
+__device__ __forceinline__ uint32_t light_and_shadow(Walker<STORE, COUNT, CRAWL>& w, const KView& v, const Hit& h) {
     bool sh = false;
     const f3 rwp = add(ld3(v.translation), mk((float)(h.region.x * kBlock), (float)(h.region.y * kBlock),
                                               (float)(h.region.z * kBlock)));
@@ -1534,7 +1522,7 @@ __device__ __forceinline__ void attach(W& w, const CrawlLds* cl) {
 // pass writes and counts it).  Crawl pass: a walk that never finishes (the
 // reference would loop forever) is 0 with only the pixel write counted, as in
 // the oracle.
-template <int STORE, int ALGO, bool COUNT, bool CRAWL, bool SPARSE = false>
+template <int STORE, int ALGO, bool COUNT, bool CRAWL>
 __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint32_t x, uint32_t l,
                                           uint32_t& bytes, uint32_t* iters = nullptr, uint2* ff = nullptr,
                                           uint32_t* dg = nullptr, const CrawlLds* cl = nullptr) {
@@ -1543,16 +1531,10 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
     if (ff) *ff = uint2{0u, 0u};
     f3 ro, rd;
     if (pixel_ray<true>(v, x, l, ro, rd)) {
-        Walker<STORE, COUNT, CRAWL, SPARSE> w(s, v);
+        Walker<STORE, COUNT, CRAWL> w(s, v);
         attach(w, cl);
         Hit h;
-        const bool hit = w.template primary<ALGO>(ro, rd, h);
-        if (!CRAWL && v.prio_esc) {
-            uint32_t m = w.iters;
-            for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
-            if (m > v.prio_esc) __builtin_amdgcn_s_setprio(2);
-        }
-        if (hit) col = light_and_shadow(w, v, h);
+        if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
         if (iters) *iters = w.iters;              // the walk's length (the work order's cost)
         bytes = w.bytes + 4u;                     // + the pixel write
         if (ff) *ff = uint2{w.ff, w.nl};
@@ -1562,7 +1544,7 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
         if (w.aborted) {
             col = 0;
             if (ff) *ff = uint2{0u, 0u};
-            if (Walker<STORE, COUNT, CRAWL, SPARSE>::kExact) {
+            if (Walker<STORE, COUNT, CRAWL>::kExact) {
                 bytes = 4u;
             } else {
                 bytes = 0u;
@@ -1653,19 +1635,18 @@ template <int ALGO, bool HI> struct TileWaves {
                                                        : (HI ? VR_LONG_WAVES_HI : VR_LONG_WAVES);
 };
 static_assert(kTilesX * kTilesY == kWavesPerTileGroup, "cost layout (vr_internal.h)");
-template <int STORE, int ALGO, bool COUNT, bool HI = false, bool SPARSE = false>
+template <int STORE, int ALGO, bool COUNT, bool HI = false>
 __global__ __launch_bounds__(64 * kTilesX * kTilesY, (TileWaves<ALGO, HI>::value)) void march_kernel(KScene s, KView v) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t bx, by;
     tile_group(v, bx, by);
-    if (v.order && blockIdx.y * gridDim.x + blockIdx.x < v.prio_head) __builtin_amdgcn_s_setprio(3);
     const uint32_t x = (bx * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
     const uint32_t l = (by * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
     uint32_t bytes = 0, iters = 0;
     if (x < v.LW && l < v.local_rows) {
         // (&iters unconditionally: a pointer chosen by `v.cost ? &iters : nullptr` keeps
         // iters in scratch -- a store and a reload per lane, 8 MB of WRITE_SIZE per C2 launch)
-        v.out[(size_t)l * v.LW + x] = shade<STORE, ALGO, COUNT, false, SPARSE>(s, v, x, l, bytes, &iters);
+        v.out[(size_t)l * v.LW + x] = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes, &iters);
     }
     if (COUNT) add_bytes(v, lane, bytes);
     if (v.cost) {                                  // the wave's walk length, for the next work order
@@ -1914,7 +1895,7 @@ hipError_t launch_order(const uint32_t* cost, uint32_t n, uint32_t columns, uint
 }
 
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream,
-                        uint32_t crawl_wgs, bool in_flight, bool sparse) {
+                        uint32_t crawl_wgs, bool in_flight) {
     uint32_t gx, gy;
     march_grid(v, gx, gy);
     dim3 grid(gx, gy);
@@ -1923,17 +1904,16 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
     const dim3 cgrid(crawl_wgs ? crawl_wgs : 64u);
     const dim3 cblock(64u * kCrawlWaves);
 #define VR_LAUNCH(ST, AL, CT) VR_LAUNCH_HI(ST, AL, CT, false)
-#define VR_LAUNCH_HI(ST, AL, CT, HI) VR_LAUNCH_SP(ST, AL, CT, HI, false)
-#define VR_LAUNCH_SP(ST, AL, CT, HI, SP)                                                          \
+#define VR_LAUNCH_HI(ST, AL, CT, HI)                                                              \
     do {                                                                                           \
-        hipLaunchKernelGGL((march_kernel<ST, AL, CT, HI, SP>), grid, block, 0, stream, s, v);      \
+        hipLaunchKernelGGL((march_kernel<ST, AL, CT, HI>), grid, block, 0, stream, s, v);          \
         if (v.defer && !kNoCrawlPass)                                                              \
             hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, cblock, 0, stream, s, v);        \
     } while (0)
 #ifdef VR_ISA_ONLY
     // ISA-inspection builds (csrc/Makefile isa1, profiles/loop_isa.py): one kernel pair
     // only, e.g. -DVR_ISA_ONLY=ALGO_LONGEST for the VCS longest-axis tile pass; never a library
-    (void)algo; (void)count; (void)store; (void)sparse;
+    (void)algo; (void)count; (void)store;
     VR_LAUNCH(STORE_VCS, VR_ISA_ONLY, false);
     return hipGetLastError();
 #endif
@@ -1941,12 +1921,7 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
     // VCS longest-axis walks; the VCS original walk is fastest at 7 waves either way)
     const bool hi = in_flight && !count;
     if (store == STORE_VCS) {
-        // (the instrumented launch keeps the dense walk: same pixels, same counted bytes)
-        if (algo == ALGO_ORIGINAL) {
-            if (count) VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, true);
-            else if (sparse) VR_LAUNCH_SP(STORE_VCS, ALGO_ORIGINAL, false, false, true);
-            else VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, false);
-        }
+        if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, false); }
         else if (hi) VR_LAUNCH_HI(STORE_VCS, ALGO_LONGEST, false, true);
         else { if (count) VR_LAUNCH(STORE_VCS, ALGO_LONGEST, true); else VR_LAUNCH(STORE_VCS, ALGO_LONGEST, false); }
     } else {
@@ -1959,7 +1934,6 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
     }
 #undef VR_LAUNCH
 #undef VR_LAUNCH_HI
-#undef VR_LAUNCH_SP
     return hipGetLastError();
 }
 

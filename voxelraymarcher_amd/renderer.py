@@ -279,22 +279,13 @@ class Occupancy(enum.IntEnum):
     IN_FLIGHT = _capi.VR_OCCUPANCY_IN_FLIGHT
 
 
-class Sparse(enum.IntEnum):
-    """vr_sparse: the VCS original walk's existence test (identical pixels).  ON reads the region's
-    cluster-existence bits first and a mask word only in a present cluster (sparse scenes); AUTO picks
-    ON for scenes with fewer than 1 in 8 cluster slots of their occupied regions present."""
-    AUTO = _capi.VR_SPARSE_AUTO
-    OFF = _capi.VR_SPARSE_OFF
-    ON = _capi.VR_SPARSE_ON
-
-
 def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
               info: VoxelSceneInfo, width: int, height: int, out: torch.Tensor, row_begin: int = 0,
               row_end: int | None = None, band_rows: int = 0, rank: int = 0, nranks: int = 1,
               counter: torch.Tensor | None = None, kernel: Kernel = Kernel.AUTO, stream=None,
               defer_cap: int = 0, schedule: Schedule = Schedule.AUTO,
               stats: torch.Tensor | None = None, occupancy: Occupancy = Occupancy.AUTO,
-              tile_cols: int = 0, deal_stride: int = 0, sparse: Sparse = Sparse.AUTO) -> torch.Tensor:
+              tile_cols: int = 0, deal_stride: int = 0) -> torch.Tensor:
     """vr_render_ex: rows [row_begin,row_end), bands of band_rows (0 = one band) dealt to nranks ranks.
     defer_cap: capacity of the crawl pass's deferral list (0 = default; small values force its overflow path).
     schedule: the tile pass's work order (Schedule); occupancy: its occupancy variant (Occupancy).
@@ -322,7 +313,6 @@ def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, 
     opts.defer_cap, opts.schedule = int(defer_cap), int(schedule)
     opts.stats_dev = c_void_p(stats.data_ptr()) if stats is not None else None
     opts.occupancy, opts.tile_cols, opts.deal_stride = int(occupancy), int(tile_cols), int(deal_stride)
-    opts.sparse = int(sparse)
     check(lib().vr_render_ex(scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
                              f3(info.translation), int(info.scale), int(width), int(height), ctypes.byref(opts),
                              c_void_p(out.data_ptr()), _stream_ptr(stream)), "vr_render_ex")
