@@ -199,12 +199,6 @@ __device__ __forceinline__ float plane_v(float o, float g, float ge) {
     else if constexpr (S < 0) return floorf(o) - kEps;
     else return next_plane_fma(o, g, ge);
 }
-// ceilf(o) / floorf(o) of a sign-specialised plane (the +-EPSILON added separately: packed)
-template <int S>
-__device__ __forceinline__ float plane_r(float o) {
-    if constexpr (S > 0) return ceilf(o);
-    else return floorf(o);
-}
 template <int S>
 __device__ __forceinline__ int32_t plane_c8(int32_t c8) {
     if constexpr (S > 0) return 8;
@@ -246,11 +240,6 @@ __device__ __forceinline__ bool crawl_voxel(float on, float c, int32_t& q) {
 #define VR_TILES_Y 1
 #endif
 constexpr uint32_t kTilesX = VR_TILES_X, kTilesY = VR_TILES_Y;
-// VR_PACKED: the VCS original walk's x/y arithmetic as packed FP32 (see the loop)
-#ifndef VR_PACKED
-#define VR_PACKED 0
-#endif
-typedef float v2f __attribute__((ext_vector_type(2)));
 // VR_UNIFORM_SKIP: the cluster-skip planes and their selects are computed only in
 // wave-iterations where some lane stands in an absent cluster (one uniform branch on
 // the ballot).  In C2, 61 % of the primary and 60 % of the shadow wave-iterations
@@ -488,24 +477,9 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                         // skips (a scalar branch; -2 VALU per iteration without a skip).
                         const bool okw = __builtin_amdgcn_ballot_w64(!walk_ok) == 0;
                         VR_DIAG_COUNT((SHADOW ? 4 : 0) + (SX == 0 ? 1 : 0));   // walk entries
-#if VR_PACKED
-                        // Packed FP32 (VR_PACKED): the x and y halves of the walk's arithmetic --
-                        // plane offsets, numerators, the three-op division, the step -- as
-                        // v_pk_{add,mul,fma}_f32 on register pairs (two IEEE fp32 ops per
-                        // instruction, rounded exactly as the scalar ones: the same pixels).
-                        v2f oxy = {o.x, o.y};
-                        float oz = o.z;
-                        const v2f dxy = EQ ? v2f{d.x, d.x} : v2f{d.x, d.y};
-                        const v2f rrxy = {rx.r, ry.r}, rdxy = {rx.d, ry.d};
-                        const v2f exy = {ex, ey};
-#endif
                         for (;;) {
                             VR_DIAG_COUNT((SHADOW ? 6 : 2) + (SX == 0 ? 1 : 0));   // loop iterations
-#if VR_PACKED
-                            const int32_t vx = f2i(oxy.x), vy = f2i(oxy.y), vz = f2i(oz);
-#else
                             const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-#endif
                             this->count(4);
                             const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
                             if constexpr (CRAWL) {
@@ -521,82 +495,6 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                                                                       (moff | (wi << 3)));
                             }
                             __builtin_amdgcn_sched_barrier(0);   // issue the load before the planes
-#if VR_PACKED
-                            // both candidate planes while the mask word is in flight (see below)
-                            v2f vXY;
-                            float vZ;
-                            if constexpr (SX == 0) {
-                                vXY = v2f{plane_v<0>(oxy.x, gx, ex), plane_v<0>(oxy.y, gy, ey)};
-                                vZ = plane_v<0>(oz, gz, ez);
-                            } else {
-                                vXY = v2f{plane_r<SX>(oxy.x), plane_r<SY>(oxy.y)} + exy;   // ceil/floor +- EPSILON
-                                vZ = plane_v<SZ>(oz, gz, ez);
-                            }
-                            asm("" : "+v"(vXY), "+v"(vZ), "+v"(blk.x), "+v"(blk.y));
-                            const bool skip = absent(blk);
-                            v2f nXY = vXY;
-                            float nZ = vZ;
-                            const bool any_skip = __builtin_amdgcn_ballot_w64(skip) != 0;
-                            if (any_skip) {
-                                const float cX = (float)((vx & 0x38) + plane_c8<SX>(cx8)),
-                                            cY = (float)((vy & 0x38) + plane_c8<SY>(cy8)),
-                                            cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
-                                nXY = v2f{skip ? cX : vXY.x, skip ? cY : vXY.y};
-                                nZ = skip ? cZ : vZ;
-                                asm volatile("" : "+v"(nXY), "+v"(nZ));
-                            }
-                            const bool chk = !kPos && (!okw || any_skip);   // (uniform)
-                            bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
-                            const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)blk.x, bit, 1u);
-                            found = fm != 0u;
-                            vi = blk.y + __popc(blk.x & ((1u << (bit & 31u)) - 1u));
-                            if (COUNT && !skip) this->count_bsearch(mreg + (wi & ~15u), vi, found);
-                            const v2f axy = nXY - oxy;
-                            const float az = nZ - oz;
-                            float sMin;
-                            crawl = false;
-                            if (EQ) {
-                                const float am = fminf(fabsf(axy.x), fminf(fabsf(axy.y), fabsf(az)));
-                                sMin = div_fast(am, rx);
-                                if (chk) {
-                                    const bool bad = !(am >= nlim);
-                                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                                        sMin = bad ? am / fabsf(d.x) : sMin;
-                                        crawl = bad & walk_ok & skip & (sMin == 0.0f) &
-                                                (CRAWL ? ic + 1u - (0x42800000u - kBudget) >= crawl_after : !crawl_off);
-                                        if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
-                                    }
-                                }
-                            } else {
-                                // div_fast on the pair: q = n r; q' = fma(fma(-d, q, n), r, q)
-                                const v2f q0 = axy * rrxy;
-                                v2f sXY = __builtin_elementwise_fma(__builtin_elementwise_fma(-rdxy, q0, axy), rrxy, q0);
-                                float sZ = div_fast(az, rz);
-                                if (chk) {
-                                    const bool bad = !(fminf(fabsf(axy.x), fminf(fabsf(axy.y), fabsf(az))) >= nlim);
-                                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                                        const float bX = bad ? (zx ? kInf : axy.x / d.x) : sXY.x;
-                                        const float bY = bad ? (zy ? kInf : axy.y / d.y) : sXY.y;
-                                        sXY = v2f{bX, bY};
-                                        sZ = bad ? (zz ? kInf : az / d.z) : sZ;
-                                        crawl = bad & walk_ok & skip & (fminf(sXY.x, fminf(sXY.y, sZ)) == 0.0f) &
-                                                (CRAWL ? ic + 1u - (0x42800000u - kBudget) >= crawl_after : !crawl_off);
-                                        if (CRAWL && crawl) { qx = vx; qy = vy; qz = vz; }
-                                    }
-                                }
-                                sMin = fminf(sXY.x, fminf(sXY.y, sZ));
-                                const bool vox = !skip && !found;
-                                tX = vox ? sXY.x : tX; tY = vox ? sXY.y : tY; tZ = vox ? sZ : tZ;
-                            }
-                            const float ts = bit_select(fm, -kEps, sMin) + kEps;
-                            oxy = oxy + v2f{ts, ts} * dxy;
-                            oz = oz + ts * (EQ ? d.x : d.z);
-                            asm("v_add_u32 %0, 1, %0" : "+v"(ic));
-                            const uint32_t ev = max(max(max(max(__float_as_uint(oxy.x), __float_as_uint(oxy.y)),
-                                                            __float_as_uint(oz)), ic), fm);
-                            if (ev >= 0x42800000u || crawl) break;
-#else
-                            this->count(4);
                             // both candidate planes, computed while the mask word is in
                             // flight and materialised (with the whole 8-B word: one load)
 #if VR_UNIFORM_SKIP
@@ -686,11 +584,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                             const uint32_t ev = max(max(max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)),
                                                         ic), fm);
                             if (ev >= 0x42800000u || crawl) break;
-#endif
                         }
-#if VR_PACKED
-                        o = f3{oxy.x, oxy.y, oz};
-#endif
                         this->iters = ic - (0x42800000u - kBudget);
                     };
                     const uint32_t sg = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
@@ -834,63 +728,6 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             const uint32_t foff = reg << 15;
             uint32_t fw = 0, bit = 0;
             uint32_t ic = this->iters + (0x42800000u - kBudget);   // biased count (see the VCS walk)
-#if VR_PACKED
-            // x/y halves as packed FP32 (VR_PACKED, see the VCS walk)
-            v2f oxy = {o.x, o.y};
-            float oz = o.z;
-            const v2f gxy = {gx, gy}, exy = {ex, ey};
-            const v2f dxy = EQ ? v2f{d.x, d.x} : v2f{d.x, d.y};
-            const v2f rrxy = {rx.r, ry.r}, rdxy = {rx.d, ry.d};
-            for (;;) {
-                const int32_t vx = f2i(oxy.x), vy = f2i(oxy.y), vz = f2i(oz);
-                const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
-                fw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s.ht_filter) + (foff | (wi << 2)));
-                __builtin_amdgcn_sched_barrier(0);   // issue the load before the step
-                // next_plane_fma on the pair: fma(g, ceilf(g * o), g * EPSILON)
-                const v2f gc = gxy * oxy;
-                const v2f axy = __builtin_elementwise_fma(gxy, v2f{ceilf(gc.x), ceilf(gc.y)}, exy) - oxy;
-                const float az = next_plane_fma(oz, gz, ez) - oz;
-                float sMin;
-                v2f sXY = {0.0f, 0.0f};
-                float sZ = 0.0f;
-                if (EQ) {
-                    const float am = fminf(fabsf(axy.x), fminf(fabsf(axy.y), fabsf(az)));
-                    sMin = div_fast(am, rx);
-                    if (!okw) {
-                        const bool bad = !(am >= nlim);
-                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) sMin = bad ? am / fabsf(d.x) : sMin;
-                    }
-                } else {
-                    const v2f q0 = axy * rrxy;
-                    sXY = __builtin_elementwise_fma(__builtin_elementwise_fma(-rdxy, q0, axy), rrxy, q0);
-                    sZ = div_fast(az, rz);
-                    if (!okw) {
-                        const bool bad = !(fminf(fabsf(axy.x), fminf(fabsf(axy.y), fabsf(az))) >= nlim);
-                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                            const float bX = bad ? (zx ? kInf : axy.x / d.x) : sXY.x;
-                            const float bY = bad ? (zy ? kInf : axy.y / d.y) : sXY.y;
-                            sXY = v2f{bX, bY};
-                            sZ = bad ? (zz ? kInf : az / d.z) : sZ;
-                        }
-                    }
-                    sMin = fminf(sXY.x, fminf(sXY.y, sZ));
-                }
-                this->count(8u);
-                bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
-                const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)fw, bit, 1u);   // 0 or ~0: present
-                if (!SHADOW && !EQ) {
-                    tX = fm ? tX : sXY.x; tY = fm ? tY : sXY.y; tZ = fm ? tZ : sZ;
-                }
-                const float ts = bit_select(fm, -kEps, sMin) + kEps;
-                oxy = oxy + v2f{ts, ts} * dxy;
-                oz = oz + ts * (EQ ? d.x : d.z);
-                asm("v_add_u32 %0, 1, %0" : "+v"(ic));
-                const uint32_t ev = max(max(max(max(__float_as_uint(oxy.x), __float_as_uint(oxy.y)), __float_as_uint(oz)), ic), fm);
-                if (ev >= 0x42800000u) break;
-            }
-            o = f3{oxy.x, oxy.y, oz};
-#else
-            uint32_t ic = this->iters + (0x42800000u - kBudget);   // biased count (see the VCS walk)
             for (;;) {
                 const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
                 const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
@@ -934,7 +771,6 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                 const uint32_t ev = max(max(max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)), ic), fm);
                 if (ev >= 0x42800000u) break;
             }
-#endif
             this->iters = ic - (0x42800000u - kBudget);
             // why the lane left (see the VCS walk): recomputed from VGPR values
             asm("" : "+v"(fw), "+v"(bit), "+v"(o.x), "+v"(o.y), "+v"(o.z));
