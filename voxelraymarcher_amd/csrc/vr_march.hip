@@ -727,79 +727,51 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             // the region's filter words as a 32-bit byte offset from the scene's (SGPR-base loads)
             const uint32_t foff = reg << 15;
             uint32_t fw = 0, bit = 0;
-            // specialised, as the VCS walk, for the direction signs the wave's lanes share (the
-            // planes then need no sign multiplications: ceilf(o) + EPSILON / floorf(o) - EPSILON),
-            // one pass per sign pattern present; an equal-component shadow direction has one
-            auto walk = [&](auto SXc, auto SYc, auto SZc) {
-                constexpr int SX = decltype(SXc)::value, SY = decltype(SYc)::value, SZ = decltype(SZc)::value;
-                uint32_t ic = this->iters + (0x42800000u - kBudget);   // biased count (see the VCS walk)
-                for (;;) {
-                    const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
-                    const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
-                    fw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s.ht_filter) + (foff | (wi << 2)));
-                    __builtin_amdgcn_sched_barrier(0);   // issue the load before the step
-                    // rayMarchVoxelGrid's voxel step (Renderer.cuh:318-331), while the word loads
-                    const float ax = plane_v<SX>(o.x, gx, ex) - o.x, ay = plane_v<SY>(o.y, gy, ey) - o.y,
-                                az = plane_v<SZ>(o.z, gz, ez) - o.z;
-                    float sMin, sX = 0.0f, sY = 0.0f, sZ = 0.0f;
-                    if (EQ) {                                 // see grid_original
-                        const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
-                        sMin = div_fast(am, rx);
-                        if (!okw) {
-                            const bool bad = !(am >= nlim);
-                            if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) sMin = bad ? am / fabsf(d.x) : sMin;
-                        }
-                    } else {
-                        sX = div_fast(ax, rx); sY = div_fast(ay, ry); sZ = div_fast(az, rz);
-                        if (!okw) {
-                            const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
-                            if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                                sX = bad ? (zx ? kInf : ax / d.x) : sX;
-                                sY = bad ? (zy ? kInf : ay / d.y) : sY;
-                                sZ = bad ? (zz ? kInf : az / d.z) : sZ;
-                            }
-                        }
-                        sMin = fminf(sX, fminf(sY, sZ));
+            uint32_t ic = this->iters + (0x42800000u - kBudget);   // biased count (see the VCS walk)
+            for (;;) {
+                const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
+                const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
+                fw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s.ht_filter) + (foff | (wi << 2)));
+                __builtin_amdgcn_sched_barrier(0);   // issue the load before the step
+                // rayMarchVoxelGrid's voxel step (Renderer.cuh:318-331), while the word loads
+                const float ax = next_plane_fma(o.x, gx, ex) - o.x, ay = next_plane_fma(o.y, gy, ey) - o.y,
+                            az = next_plane_fma(o.z, gz, ez) - o.z;
+                float sMin, sX = 0.0f, sY = 0.0f, sZ = 0.0f;
+                if (EQ) {                                 // see grid_original
+                    const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
+                    sMin = div_fast(am, rx);
+                    if (!okw) {
+                        const bool bad = !(am >= nlim);
+                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) sMin = bad ? am / fabsf(d.x) : sMin;
                     }
-                    // key1 + key2 of a key the tables do not hold; the hit's own bytes are
-                    // settled after the loop (8 or 12)
-                    this->count(8u);
-                    bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
-                    const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)fw, bit, 1u);   // 0 or ~0: present
-                    if (!SHADOW && !EQ) {                     // a non-hit step: its t values feed the normal
-                        tX = fm ? tX : sX; tY = fm ? tY : sY; tZ = fm ? tZ : sZ;
+                } else {
+                    sX = div_fast(ax, rx); sY = div_fast(ay, ry); sZ = div_fast(az, rz);
+                    if (!okw) {
+                        const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
+                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                            sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                            sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                            sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                        }
                     }
-                    // a hit keeps o unstepped: step length (-EPSILON) + EPSILON = +0 (see the VCS walk)
-                    const float ts = bit_select(fm, -kEps, sMin) + kEps;
-                    o = EQ ? add(o, f3{ts * d.x, ts * d.x, ts * d.x}) : add(o, scl(ts, d));
-                    asm("v_add_u32 %0, 1, %0" : "+v"(ic));      // (see the VCS walk)
-                    const uint32_t ev = max(max(max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)), ic), fm);
-                    if (ev >= 0x42800000u) break;
+                    sMin = fminf(sX, fminf(sY, sZ));
                 }
-                this->iters = ic - (0x42800000u - kBudget);
-            };
-            {
-                const uint32_t sg = (px ? 1u : 0u) | (py ? 2u : 0u) | (pz ? 4u : 0u);
-                using N = Sgn<-1>;
-                using P = Sgn<1>;
-                bool todo = true;
-                while (todo) {
-                    const uint32_t pat = __builtin_amdgcn_readfirstlane(sg);
-                    if (sg == pat) {
-                        todo = false;
-                        switch (pat) {
-                        case 0: walk(N{}, N{}, N{}); break;
-                        case 7: walk(P{}, P{}, P{}); break;
-                        case 1: if (!EQ) walk(P{}, N{}, N{}); break;
-                        case 2: if (!EQ) walk(N{}, P{}, N{}); break;
-                        case 3: if (!EQ) walk(P{}, P{}, N{}); break;
-                        case 4: if (!EQ) walk(N{}, N{}, P{}); break;
-                        case 5: if (!EQ) walk(P{}, N{}, P{}); break;
-                        default: if (!EQ) walk(N{}, P{}, P{}); break;
-                        }
-                    }
+                // key1 + key2 of a key the tables do not hold; the hit's own bytes are
+                // settled after the loop (8 or 12)
+                this->count(8u);
+                bit = this->word_bit5((uint32_t)vy, (uint32_t)vz);
+                const uint32_t fm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)fw, bit, 1u);   // 0 or ~0: present
+                if (!SHADOW && !EQ) {                     // a non-hit step: its t values feed the normal
+                    tX = fm ? tX : sX; tY = fm ? tY : sY; tZ = fm ? tZ : sZ;
                 }
+                // a hit keeps o unstepped: step length (-EPSILON) + EPSILON = +0 (see the VCS walk)
+                const float ts = bit_select(fm, -kEps, sMin) + kEps;
+                o = EQ ? add(o, f3{ts * d.x, ts * d.x, ts * d.x}) : add(o, scl(ts, d));
+                asm("v_add_u32 %0, 1, %0" : "+v"(ic));      // (see the VCS walk)
+                const uint32_t ev = max(max(max(max(__float_as_uint(o.x), __float_as_uint(o.y)), __float_as_uint(o.z)), ic), fm);
+                if (ev >= 0x42800000u) break;
             }
+            this->iters = ic - (0x42800000u - kBudget);
             // why the lane left (see the VCS walk): recomputed from VGPR values
             asm("" : "+v"(fw), "+v"(bit), "+v"(o.x), "+v"(o.y), "+v"(o.z));
             if (!__builtin_amdgcn_ubfe(fw, bit, 1u)) {
