@@ -477,9 +477,6 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                         // skips (a scalar branch; -2 VALU per iteration without a skip).
                         const bool okw = __builtin_amdgcn_ballot_w64(!walk_ok) == 0;
                         VR_DIAG_COUNT((SHADOW ? 4 : 0) + (SX == 0 ? 1 : 0));   // walk entries
-#if VR_UNIFORM_SKIP == 2
-                        bool pskip = false;          // (wave-uniform) see the predicted form below
-#endif
                         for (;;) {
                             VR_DIAG_COUNT((SHADOW ? 6 : 2) + (SX == 0 ? 1 : 0));   // loop iterations
                             const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
@@ -500,45 +497,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                             __builtin_amdgcn_sched_barrier(0);   // issue the load before the planes
                             // both candidate planes, computed while the mask word is in
                             // flight and materialised (with the whole 8-B word: one load)
-#if VR_UNIFORM_SKIP == 2
-                            // Predicted form: when every active lane skipped in the previous
-                            // wave-iteration (pskip, wave-uniform), only the cluster-skip planes are
-                            // made ahead of the mask word; the voxel planes follow only if some lane
-                            // turns out to stand in a present cluster.  Otherwise as form 1.
-                            float nX, nY, nZ;
-                            bool skip, any_skip;
-                            if (pskip) {
-                                float cX = (float)((vx & 0x38) + plane_c8<SX>(cx8)), cY = (float)((vy & 0x38) + plane_c8<SY>(cy8)),
-                                      cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
-                                asm("" : "+v"(cX), "+v"(cY), "+v"(cZ), "+v"(blk.x), "+v"(blk.y));
-                                skip = absent(blk);
-                                const uint64_t bs = __builtin_amdgcn_ballot_w64(skip);
-                                const uint64_t ex_ = __builtin_amdgcn_read_exec();
-                                any_skip = bs != 0;
-                                pskip = bs == ex_;
-                                nX = cX; nY = cY; nZ = cZ;
-                                if (bs != ex_) {
-                                    const float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey),
-                                                vZ = plane_v<SZ>(o.z, gz, ez);
-                                    nX = skip ? cX : vX; nY = skip ? cY : vY; nZ = skip ? cZ : vZ;
-                                    asm volatile("" : "+v"(nX), "+v"(nY), "+v"(nZ));
-                                }
-                            } else {
-                                float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey), vZ = plane_v<SZ>(o.z, gz, ez);
-                                asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(blk.x), "+v"(blk.y));
-                                skip = absent(blk);
-                                const uint64_t bs = __builtin_amdgcn_ballot_w64(skip);
-                                any_skip = bs != 0;
-                                pskip = bs == __builtin_amdgcn_read_exec();
-                                nX = vX; nY = vY; nZ = vZ;
-                                if (any_skip) {
-                                    float cX = (float)((vx & 0x38) + plane_c8<SX>(cx8)), cY = (float)((vy & 0x38) + plane_c8<SY>(cy8)),
-                                          cZ = (float)((vz & 0x38) + plane_c8<SZ>(cz8));
-                                    nX = skip ? cX : vX; nY = skip ? cY : vY; nZ = skip ? cZ : vZ;
-                                    asm volatile("" : "+v"(nX), "+v"(nY), "+v"(nZ));
-                                }
-                            }
-#elif VR_UNIFORM_SKIP
+#if VR_UNIFORM_SKIP
                             float vX = plane_v<SX>(o.x, gx, ex), vY = plane_v<SY>(o.y, gy, ey), vZ = plane_v<SZ>(o.z, gz, ez);
                             asm("" : "+v"(vX), "+v"(vY), "+v"(vZ), "+v"(blk.x), "+v"(blk.y));
                             const bool skip = absent(blk);
