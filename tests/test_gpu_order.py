@@ -108,3 +108,28 @@ def test_schedules_render_identical_pixels():
     with pytest.raises(vr.VrError):
         vr.render_ex(scene, vr.RayMarchAlgorithm.ORIGINAL, cam, lit, info, W, H, out, schedule=7)
     scene.close()
+
+
+@pytest.mark.parametrize("store", ["vcs", "hashtable"])
+def test_lane_order_ragged_frames(store):
+    # the lane order (vr_march.hip lane_pixel) deals each 16x16 block's pixels to its four
+    # waves heaviest first once a slot has recorded the grid's per-pixel walk lengths: ragged
+    # frames (partial blocks at the right edge, an odd number of tile-group rows whose last
+    # block row keeps the identity order) must render the same pixels with it as without
+    cfg = vr.CONFIGS["C1"]
+    xyz, rgb = cfg.voxels()
+    scene = vr.create_scene(xyz, rgb, vr.parse_storage(store))
+    lit = vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    for W, H in [(200, 37), (17, 250), (333, 41)]:
+        cam = vr.Camera.reference(W, H)
+        for algo in (vr.RayMarchAlgorithm.ORIGINAL, vr.RayMarchAlgorithm.LONGEST_AXIS):
+            ref = None
+            for i in range(40):       # past two uses of each of the ring's 16 slots
+                out = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
+                vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out)
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = out.clone()
+                assert torch.equal(out, ref), (store, W, H, algo.name, i)
+    scene.close()

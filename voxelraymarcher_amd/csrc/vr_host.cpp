@@ -558,6 +558,14 @@ struct SlotRing {
             uint32_t* order = nullptr;     // one word per tile group
             uint32_t cap = 0, gx = 0, gy = 0, age = 0;
             bool valid = false;
+            // the lane order (vr_march.hip lane_pixel): per-pixel walk lengths and, per 16x16
+            // block, its pixels heaviest first, for a grid of lgx x lgy
+            uint32_t* pcost = nullptr;     // one word per pixel of the view
+            uint8_t* perm = nullptr;       // 256 bytes per block
+            size_t pcap = 0, bcap = 0;
+            uint32_t lgx = 0, lgy = 0, lage = 0;
+            bool lvalid = false;
+            bool relaned = false;          // the lane order changed after the work order's costs
         };
         std::vector<Order> ord;
         bool any = false;                  // the device's previous launch: its stream and slot
@@ -673,6 +681,14 @@ bool in_flight_occupancy() {
     }();
     return on;
 }
+// VR_LANE_ORDER=0 (A/B runs): 8x8 tiles, no per-pixel lane order.
+bool lane_order_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("VR_LANE_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 bool order_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("VR_ORDER");
@@ -755,8 +771,45 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         }
         const bool match = O.valid && O.gx == gx && O.gy == gy;
         v.order = match ? O.order : nullptr;
-        remake = !match || ++O.age >= order_refresh();
+        // (a work order made from costs walked under another lane order is remade: the lane
+        // order moves the heavy pixels of a block into one of its two tile groups)
+        remake = !match || O.relaned || ++O.age >= order_refresh();
         v.cost = remake ? O.cost : nullptr;
+    }
+    // The lane order, kept like the work order but for every schedule: this slot's if it was
+    // made for this grid, remade from this launch's per-pixel walk lengths when missing or
+    // every order_refresh() uses.  It permutes pixels within 16x16 blocks only, so any view
+    // of the same grid renders the same pixels with it.
+    bool relane = false;
+    const size_t npx = (size_t)v.LW * v.local_rows, nblk = (size_t)gx * ((gy + 1u) / 2u);
+    if (lane_order_enabled() && n != 0) {
+        if (npx > O.pcap || nblk > O.bcap) {
+            hipError_t e = hipSuccess;
+            if (O.pcost) e = hipFreeAsync(O.pcost, st);
+            if (O.perm) {
+                const hipError_t e2 = hipFreeAsync(O.perm, st);
+                if (e == hipSuccess) e = e2;
+            }
+            O.pcost = nullptr;
+            O.perm = nullptr;
+            O.pcap = O.bcap = 0;
+            O.lvalid = false;
+            if (e == hipSuccess) e = hipMallocAsync((void**)&O.pcost, sizeof(uint32_t) * npx, st);
+            if (e == hipSuccess) e = hipMallocAsync((void**)&O.perm, 256 * nblk, st);
+            if (e != hipSuccess) {
+                if (O.pcost) (void)hipFreeAsync(O.pcost, st);
+                if (O.perm) (void)hipFreeAsync(O.perm, st);
+                O.pcost = nullptr;
+                O.perm = nullptr;
+                return hip_fail(e, "lane order buffers");
+            }
+            O.pcap = npx;
+            O.bcap = nblk;
+        }
+        const bool match = O.lvalid && O.lgx == gx && O.lgy == gy;
+        v.perm = match ? O.perm : nullptr;
+        relane = !match || ++O.lage >= order_refresh();
+        v.pcost = relane ? O.pcost : nullptr;
     }
     // crawl pass grid from the records an earlier launch deferred (a hint: any grid renders
     // the same pixels)
@@ -767,7 +820,22 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     const bool hi = occupancy == VR_OCCUPANCY_IN_FLIGHT ||
                     (occupancy == VR_OCCUPANCY_AUTO && !alone && in_flight_occupancy());
     hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs, hi);
-    if (e == hipSuccess && remake) {
+    // The lane order first: when the slot has work-order buffers for this grid, perm_kernel
+    // also writes the waves' costs under the new lane order and the work order is remade from
+    // them at once -- an order made from costs walked under another lane order puts the light
+    // half of a block first as often as the heavy one (C2 lone launch 0.125 -> 0.185 ms with
+    // it, 0.116 without, profiles/r05/lane_order/).
+    bool with_costs = false;
+    if (e == hipSuccess && relane) {
+        with_costs = order_enabled() && O.cost && O.cap >= n;
+        e = vr::launch_perm(O.pcost, v.LW, v.local_rows, gx, gy, O.perm, with_costs ? O.cost : nullptr, st);
+        O.lvalid = e == hipSuccess;
+        O.relaned = !with_costs;
+        O.lgx = gx;
+        O.lgy = gy;
+        O.lage = 0;
+    }
+    if (e == hipSuccess && (remake || with_costs)) {
         // (on a side stream instead -- one more stream than the box's 4 hardware queues
         // serialised the two render streams: C2 0.1124 -> 0.1277 ms per frame in flight,
         // profiles/r03/ab_order_C2_C3.txt)
@@ -790,6 +858,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         O.gx = gx;
         O.gy = gy;
         O.age = 0;
+        O.relaned = false;
     }
     // (on a failed launch the slot is still fenced: a kernel of it may be queued)
     rc = lease.release(st);

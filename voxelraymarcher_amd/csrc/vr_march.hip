@@ -279,6 +279,30 @@ __device__ __forceinline__ void tile_group(const KView& v, uint32_t& bx, uint32_
     }
 }
 
+// The pixel (local column x, local row l) of this tile-pass lane.  Without a lane order
+// (KView::perm null) wave w of tile group (bx, by) is the 8x8 tile (2 bx + w, by).  With one,
+// the two tile groups (bx, 2B) and (bx, 2B + 1) share the 16x16 pixel block (bx, B): its 256
+// pixels are dealt to their four waves heaviest first (perm_kernel, from the walk lengths an
+// earlier launch of the view recorded), so a wave's lanes walk about equally far and finish
+// together -- C2: 24 % fewer wave-iterations for the same per-lane work (the oracle's
+// per-pixel counts, profiles/r05/lane_sort_sim.py, lane_order/).  Slot q = 2 (by & 1) + w of the block,
+// lane i: byte perm[block * 256 + 64 q + i] = (pixel row << 4 | pixel column) in the block.
+constexpr bool kLaneOrder = kTilesX == 2 && kTilesY == 1;   // (other tile shapes ignore perm)
+__device__ __forceinline__ void lane_pixel(const KView& v, uint32_t& x, uint32_t& l) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t bx, by;
+    tile_group(v, bx, by);
+    if (kLaneOrder && v.perm) {
+        const uint32_t q = ((by & 1u) << 1) | wave;
+        const uint32_t p = v.perm[((size_t)((by >> 1) * gridDim.x + bx) << 8) + (q << 6) + lane];
+        x = bx * 16u + (p & 15u);
+        l = (by >> 1) * 16u + (p >> 4);
+    } else {
+        x = (bx * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
+        l = (by * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
+    }
+}
+
 // CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
 // crawling ray reserves an entry in the launch's deferral list and unwinds.
 // kExact (the crawl pass): every walk runs to its end here, and a loop round that
@@ -646,13 +670,10 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                         if (idx < v.defer_cap) {
                             // (the tile pass writes this pixel as 0; the crawl pass,
                             // which runs after it, overwrites it and counts its bytes)
-                            // (the pixel again from the workgroup's tile group: not kept live
-                            // through the walk)
-                            const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-                            uint32_t tbx, tby;
-                            tile_group(v, tbx, tby);
-                            const uint32_t px_ = (tbx * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
-                            const uint32_t pl_ = (tby * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
+                            // (the pixel again from the workgroup's tile group and the lane
+                            // order: not kept live through the walk)
+                            uint32_t px_, pl_;
+                            lane_pixel(v, px_, pl_);
                             uint32_t* r = v.defer + 4 + (size_t)idx * kDeferRecWords;
                             r[0] = (pl_ << 16) | px_;
                             r[1] = (SHADOW ? 1u : 0u) | this->ctx;
@@ -1638,21 +1659,92 @@ static_assert(kTilesX * kTilesY == kWavesPerTileGroup, "cost layout (vr_internal
 template <int STORE, int ALGO, bool COUNT, bool HI = false>
 __global__ __launch_bounds__(64 * kTilesX * kTilesY, (TileWaves<ALGO, HI>::value)) void march_kernel(KScene s, KView v) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t bx, by;
-    tile_group(v, bx, by);
-    const uint32_t x = (bx * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
-    const uint32_t l = (by * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
+    uint32_t x, l;
+    lane_pixel(v, x, l);
     uint32_t bytes = 0, iters = 0;
     if (x < v.LW && l < v.local_rows) {
         // (&iters unconditionally: a pointer chosen by `v.cost ? &iters : nullptr` keeps
         // iters in scratch -- a store and a reload per lane, 8 MB of WRITE_SIZE per C2 launch)
         v.out[(size_t)l * v.LW + x] = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes, &iters);
+        if (v.pcost) v.pcost[(size_t)l * v.LW + x] = iters;    // the pixel's walk length, for the next lane order
     }
     if (COUNT) add_bytes(v, lane, bytes);
     if (v.cost) {                                  // the wave's walk length, for the next work order
         for (int off = 32; off > 0; off >>= 1) iters = max(iters, (uint32_t)__shfl_xor((int)iters, off, 64));
-        if (lane == 0) v.cost[(by * gridDim.x + bx) * kWavesPerTileGroup + wave] = iters;
+        if (lane == 0) {
+            uint32_t bx, by;
+            tile_group(v, bx, by);
+            v.cost[(by * gridDim.x + bx) * kWavesPerTileGroup + wave] = iters;
+        }
     }
+}
+
+// The lane order of one 16x16 pixel block (see lane_pixel): its 256 pixels ranked by the walk
+// length an earlier launch recorded (KView::pcost), heaviest first.  Keys (length << 8 |
+// pixel) are all distinct.  Each wave sorts its 64 keys with a bitonic network of lane
+// shuffles (no barriers); a key's rank in the block is its rank in its wave plus, for each
+// other wave, the number of that wave's sorted keys above it (binary search in LDS).  The
+// 256 pixel bytes are gathered in LDS and stored as 64 words.  A block whose second
+// tile-group row lies past the grid keeps the identity order (its one tile group renders its
+// own pixels).  With cost non-null the kernel also writes each wave's walk length under the
+// new lane order (KView::cost's layout: the key at rank 64 q is quarter q's maximum), so the
+// work order made from them next matches the lane order.
+__global__ __launch_bounds__(256) void perm_kernel(const uint32_t* __restrict__ pcost, uint32_t LW, uint32_t rows,
+                                                   uint32_t gx, uint32_t gy, uint8_t* __restrict__ perm,
+                                                   uint32_t* __restrict__ cost) {
+    __shared__ uint32_t sorted[256];
+    __shared__ uint32_t bytes[64];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    const uint32_t bx = blockIdx.x % gx, B = blockIdx.x / gx;
+    uint32_t* out = reinterpret_cast<uint32_t*>(perm + ((size_t)blockIdx.x << 8));
+    const uint32_t x = bx * 16u + (t & 15u), l = B * 16u + (t >> 4);
+    const uint32_t c = (x < LW && l < rows) ? min(pcost[(size_t)l * LW + x], 0xFFFFFFu) : 0u;
+    if (2u * B + 1u >= gy) {
+        if (cost) {                 // the two 8x8 tiles of tile group (bx, 2B): the quarter maxima
+            if (t < 2u) sorted[t] = 0u;
+            __syncthreads();
+            if ((t >> 4) < 8u) atomicMax(&sorted[(t & 15u) >> 3], c);
+            __syncthreads();
+            if (t < 2u) cost[((2u * B) * gx + bx) * kWavesPerTileGroup + t] = sorted[t];
+        }
+        if (t < 64u) {              // identity: slot 64 q + i -> pixel row 8 (q >> 1) + i / 8, column 8 (q & 1) + i % 8
+            uint32_t w = 0;
+            for (uint32_t k = 0; k < 4u; ++k) {
+                const uint32_t j = 4u * t + k, q = j >> 6, i = j & 63u;
+                w |= ((((q >> 1) * 8u + (i >> 3)) << 4) | ((q & 1u) * 8u + (i & 7u))) << (8u * k);
+            }
+            out[t] = w;
+        }
+        return;
+    }
+    uint32_t key = (c << 8) | t;
+    for (uint32_t size = 2; size <= 64u; size <<= 1) {
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            const uint32_t other = (uint32_t)__shfl_xor((int)key, (int)stride, 64);
+            const bool keep_max = ((lane & stride) == 0u) == ((lane & size) == 0u);
+            key = keep_max ? max(key, other) : min(key, other);
+        }
+    }
+    sorted[t] = key;                // lane i of wave w: the wave's i-th largest key
+    __syncthreads();
+    uint32_t rank = lane;
+    for (uint32_t o = 1; o < 4u; ++o) {
+        const uint32_t* s = sorted + (((wave + o) & 3u) << 6);
+        uint32_t lo = 0, hi = 64;   // the number of s's keys above key (s descending)
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s[mid] > key) lo = mid + 1u;
+            else hi = mid;
+        }
+        rank += lo;
+    }
+    reinterpret_cast<uint8_t*>(bytes)[rank] = (uint8_t)(key & 0xFFu);
+    if (cost && (rank & 63u) == 0u) {
+        const uint32_t q = rank >> 6;
+        cost[((2u * B + (q >> 1)) * gx + bx) * kWavesPerTileGroup + (q & 1u)] = key >> 8;
+    }
+    __syncthreads();
+    if (t < 64u) out[t] = bytes[t];
 }
 
 // Heaviest tiles first: a counting sort of the tile groups by the cost an earlier
@@ -1886,6 +1978,14 @@ constexpr bool kNoCrawlPass = false;
 void march_grid(const KView& v, uint32_t& columns, uint32_t& rows) {
     columns = (v.LW + 8u * kTilesX - 1u) / (8u * kTilesX);
     rows = (v.local_rows + 8u * kTilesY - 1u) / (8u * kTilesY);
+}
+
+hipError_t launch_perm(const uint32_t* pcost, uint32_t LW, uint32_t rows, uint32_t gx, uint32_t gy, uint8_t* perm,
+                       uint32_t* cost, hipStream_t stream) {
+    const uint32_t nb = gx * ((gy + 1u) / 2u);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(perm_kernel, dim3(nb), dim3(256), 0, stream, pcost, LW, rows, gx, gy, perm, cost);
+    return hipGetLastError();
 }
 
 hipError_t launch_order(const uint32_t* cost, uint32_t n, uint32_t columns, uint32_t* order, hipStream_t stream) {
