@@ -561,7 +561,7 @@ struct SlotRing {
             // the lane order (vr_march.hip lane_pixel): per-pixel walk lengths and, per 16x16
             // block, its pixels heaviest first, for a grid of lgx x lgy
             uint32_t* pcost = nullptr;     // one word per pixel of the view
-            uint8_t* perm = nullptr;       // 256 bytes per block
+            uint8_t* perm = nullptr;       // vr::perm_bytes(lgx, lgy)
             size_t pcap = 0, bcap = 0;
             uint32_t lgx = 0, lgy = 0, lage = 0;
             bool lvalid = false;
@@ -781,9 +781,9 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // every order_refresh() uses.  It permutes pixels within 16x16 blocks only, so any view
     // of the same grid renders the same pixels with it.
     bool relane = false;
-    const size_t npx = (size_t)v.LW * v.local_rows, nblk = (size_t)gx * ((gy + 1u) / 2u);
+    const size_t npx = (size_t)v.LW * v.local_rows, nperm = vr::perm_bytes(gx, gy);
     if (lane_order_enabled() && n != 0) {
-        if (npx > O.pcap || nblk > O.bcap) {
+        if (npx > O.pcap || nperm > O.bcap) {
             hipError_t e = hipSuccess;
             if (O.pcost) e = hipFreeAsync(O.pcost, st);
             if (O.perm) {
@@ -795,7 +795,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
             O.pcap = O.bcap = 0;
             O.lvalid = false;
             if (e == hipSuccess) e = hipMallocAsync((void**)&O.pcost, sizeof(uint32_t) * npx, st);
-            if (e == hipSuccess) e = hipMallocAsync((void**)&O.perm, 256 * nblk, st);
+            if (e == hipSuccess) e = hipMallocAsync((void**)&O.perm, nperm, st);
             if (e != hipSuccess) {
                 if (O.pcost) (void)hipFreeAsync(O.pcost, st);
                 if (O.perm) (void)hipFreeAsync(O.perm, st);
@@ -804,7 +804,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
                 return hip_fail(e, "lane order buffers");
             }
             O.pcap = npx;
-            O.bcap = nblk;
+            O.bcap = nperm;
         }
         const bool match = O.lvalid && O.lgx == gx && O.lgy == gy;
         v.perm = match ? O.perm : nullptr;

@@ -129,8 +129,9 @@ struct KView {
     // loop iterations) to cost[tile * kWavesPerTileGroup + wave], tile = row * columns + column.
     const uint32_t* order;
     uint32_t* cost;
-    // Lane order (round 5, vr_march.hip lane_pixel): per 16x16 pixel block 256 bytes dealing its
-    // pixels to its four waves heaviest first (or null: 8x8 tiles); pcost (or null): each lane
+    // Lane order (round 5, vr_march.hip lane_pixel): per pixel block (16x16 by default) the slot
+    // of each pixel, dealing them to the block's waves heaviest first (or null: 8x8 tiles;
+    // vr::perm_bytes(gx, gy) bytes); pcost (or null): each lane
     // writes its pixel's walk length (loop iterations) at [l * LW + x], for the next lane order.
     const uint8_t* perm;
     uint32_t* pcost;
@@ -187,6 +188,7 @@ hipError_t launch_order(const uint32_t* cost, uint32_t n, uint32_t columns, uint
 // The lane orders of a grid of gx x gy tile groups (gx x ceil(gy / 2) 16x16 blocks) from the
 // per-pixel walk lengths a launch wrote (KView::pcost, rows x LW words); with cost non-null
 // also the waves' walk lengths under the new lane order (KView::cost's layout).
+size_t perm_bytes(uint32_t gx, uint32_t gy);   // the lane order of a gx x gy grid
 hipError_t launch_perm(const uint32_t* pcost, uint32_t LW, uint32_t rows, uint32_t gx, uint32_t gy, uint8_t* perm,
                        uint32_t* cost, hipStream_t stream);
 

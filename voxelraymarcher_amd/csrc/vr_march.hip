@@ -18,6 +18,7 @@
 #include "vr_device.h"
 
 #include <algorithm>
+#include <type_traits>
 
 // VR_DIAG (profiling builds only, profiles/wave_counts.py): wave-level execution
 // counters -- one atomic per wave per counted event, from the wave's first
@@ -281,22 +282,34 @@ __device__ __forceinline__ void tile_group(const KView& v, uint32_t& bx, uint32_
 
 // The pixel (local column x, local row l) of this tile-pass lane.  Without a lane order
 // (KView::perm null) wave w of tile group (bx, by) is the 8x8 tile (2 bx + w, by).  With one,
-// the two tile groups (bx, 2B) and (bx, 2B + 1) share the 16x16 pixel block (bx, B): its 256
-// pixels are dealt to their four waves heaviest first (perm_kernel, from the walk lengths an
-// earlier launch of the view recorded), so a wave's lanes walk about equally far and finish
-// together -- C2: 24 % fewer wave-iterations for the same per-lane work (the oracle's
-// per-pixel counts, profiles/r05/lane_sort_sim.py, lane_order/).  Slot q = 2 (by & 1) + w of the block,
-// lane i: byte perm[block * 256 + 64 q + i] = (pixel row << 4 | pixel column) in the block.
+// the tile groups of a kLaneBlock x kLaneBlock pixel block share its pixels: they are dealt
+// to the block's waves heaviest first (perm_kernel, from the walk lengths an earlier launch
+// of the view recorded), so a wave's lanes walk about equally far and finish together --
+// 16x16 blocks, C2: 24 % fewer wave-iterations for the same per-lane work (the oracle's
+// per-pixel counts, profiles/r05/lane_sort_sim.py, lane_order/).  Slot q of a block is wave
+// w of its tile group (bx mod kLbX, by mod kLbY) in row-major order, q = 2 (tile group) + w;
+// lane i of slot q renders pixel perm[block * kLanePixels + 64 q + i] = (row * kLaneBlock +
+// column) of the block.  Blocks cut by the grid's edge keep the 8x8 tiles.
+#ifndef VR_LANE_BLOCK
+#define VR_LANE_BLOCK 16
+#endif
+constexpr uint32_t kLaneBlock = VR_LANE_BLOCK;
+static_assert(kLaneBlock == 16 || kLaneBlock == 32, "lane block: 16 or 32 pixels");
+constexpr uint32_t kLanePixels = kLaneBlock * kLaneBlock;
+constexpr uint32_t kLbX = kLaneBlock / (8u * kTilesX), kLbY = kLaneBlock / (8u * kTilesY);
+using PermT = std::conditional<kLaneBlock == 16, uint8_t, uint16_t>::type;
 constexpr bool kLaneOrder = kTilesX == 2 && kTilesY == 1;   // (other tile shapes ignore perm)
 __device__ __forceinline__ void lane_pixel(const KView& v, uint32_t& x, uint32_t& l) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t bx, by;
     tile_group(v, bx, by);
-    if (kLaneOrder && v.perm) {
-        const uint32_t q = ((by & 1u) << 1) | wave;
-        const uint32_t p = v.perm[((size_t)((by >> 1) * gridDim.x + bx) << 8) + (q << 6) + lane];
-        x = bx * 16u + (p & 15u);
-        l = (by >> 1) * 16u + (p >> 4);
+    const uint32_t BX = bx / kLbX, BY = by / kLbY;
+    if (kLaneOrder && v.perm && (BX + 1u) * kLbX <= gridDim.x && (BY + 1u) * kLbY <= gridDim.y) {
+        const uint32_t q = ((by % kLbY) * kLbX + bx % kLbX) * kTilesX + wave;
+        const uint32_t blk = BY * ((gridDim.x + kLbX - 1u) / kLbX) + BX;
+        const uint32_t p = reinterpret_cast<const PermT*>(v.perm)[(size_t)blk * kLanePixels + q * 64u + lane];
+        x = BX * kLaneBlock + p % kLaneBlock;
+        l = BY * kLaneBlock + p / kLaneBlock;
     } else {
         x = (bx * kTilesX + wave % kTilesX) * 8u + (lane & 7u);
         l = (by * kTilesY + wave / kTilesX) * 8u + (lane >> 3);
@@ -1679,45 +1692,43 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, (TileWaves<ALGO, HI>::value
     }
 }
 
-// The lane order of one 16x16 pixel block (see lane_pixel): its 256 pixels ranked by the walk
-// length an earlier launch recorded (KView::pcost), heaviest first.  Keys (length << 8 |
-// pixel) are all distinct.  Each wave sorts its 64 keys with a bitonic network of lane
-// shuffles (no barriers); a key's rank in the block is its rank in its wave plus, for each
-// other wave, the number of that wave's sorted keys above it (binary search in LDS).  The
-// 256 pixel bytes are gathered in LDS and stored as 64 words.  A block whose second
-// tile-group row lies past the grid keeps the identity order (its one tile group renders its
-// own pixels).  With cost non-null the kernel also writes each wave's walk length under the
-// new lane order (KView::cost's layout: the key at rank 64 q is quarter q's maximum), so the
-// work order made from them next matches the lane order.
-__global__ __launch_bounds__(256) void perm_kernel(const uint32_t* __restrict__ pcost, uint32_t LW, uint32_t rows,
-                                                   uint32_t gx, uint32_t gy, uint8_t* __restrict__ perm,
-                                                   uint32_t* __restrict__ cost) {
-    __shared__ uint32_t sorted[256];
-    __shared__ uint32_t bytes[64];
+// The lane order of one pixel block (see lane_pixel): its kLanePixels pixels ranked by the
+// walk length an earlier launch recorded (KView::pcost), heaviest first, one thread per pixel.
+// Keys (length << log2(kLanePixels) | pixel) are all distinct.  Each wave sorts its 64 keys
+// with a bitonic network of lane shuffles (no barriers); a key's rank in the block is its
+// rank in its wave plus, for each other wave, the number of that wave's sorted keys above it
+// (independent binary searches in LDS).  The block's slots are gathered in LDS and stored as
+// words.  With cost non-null the kernel also writes each wave's walk length under the new
+// lane order (KView::cost's layout: the key at rank 64 q is slot q's maximum; blocks cut by
+// the grid's edge keep the 8x8 tiles and write each tile's maximum), so the work order made
+// from them next matches the lane order.
+constexpr uint32_t kLaneShift = kLaneBlock == 16 ? 8u : 10u;
+__global__ __launch_bounds__(kLanePixels) void perm_kernel(const uint32_t* __restrict__ pcost, uint32_t LW,
+                                                           uint32_t rows, uint32_t gx, uint32_t gy,
+                                                           uint8_t* __restrict__ perm, uint32_t* __restrict__ cost) {
+    constexpr uint32_t kWaves = kLanePixels / 64u, kTiles = (kLaneBlock / 8u) * (kLaneBlock / 8u);
+    __shared__ uint32_t sorted[kLanePixels];
+    __shared__ __attribute__((aligned(16))) PermT slots[kLanePixels];
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    const uint32_t bx = blockIdx.x % gx, B = blockIdx.x / gx;
-    uint32_t* out = reinterpret_cast<uint32_t*>(perm + ((size_t)blockIdx.x << 8));
-    const uint32_t x = bx * 16u + (t & 15u), l = B * 16u + (t >> 4);
-    const uint32_t c = (x < LW && l < rows) ? min(pcost[(size_t)l * LW + x], 0xFFFFFFu) : 0u;
-    if (2u * B + 1u >= gy) {
-        if (cost) {                 // the two 8x8 tiles of tile group (bx, 2B): the quarter maxima
-            if (t < 2u) sorted[t] = 0u;
+    const uint32_t nbx = (gx + kLbX - 1u) / kLbX, BX = blockIdx.x % nbx, BY = blockIdx.x / nbx;
+    const uint32_t px = t % kLaneBlock, py = t / kLaneBlock;
+    const uint32_t x = BX * kLaneBlock + px, l = BY * kLaneBlock + py;
+    const uint32_t c = (x < LW && l < rows) ? min(pcost[(size_t)l * LW + x], (1u << (32u - kLaneShift)) - 1u) : 0u;
+    if ((BX + 1u) * kLbX > gx || (BY + 1u) * kLbY > gy) {
+        if (cost) {                 // the block's 8x8 tiles that exist: their maxima
+            if (t < kTiles) sorted[t] = 0u;
             __syncthreads();
-            if ((t >> 4) < 8u) atomicMax(&sorted[(t & 15u) >> 3], c);
+            atomicMax(&sorted[(py >> 3) * (kLaneBlock / 8u) + (px >> 3)], c);
             __syncthreads();
-            if (t < 2u) cost[((2u * B) * gx + bx) * kWavesPerTileGroup + t] = sorted[t];
-        }
-        if (t < 64u) {              // identity: slot 64 q + i -> pixel row 8 (q >> 1) + i / 8, column 8 (q & 1) + i % 8
-            uint32_t w = 0;
-            for (uint32_t k = 0; k < 4u; ++k) {
-                const uint32_t j = 4u * t + k, q = j >> 6, i = j & 63u;
-                w |= ((((q >> 1) * 8u + (i >> 3)) << 4) | ((q & 1u) * 8u + (i & 7u))) << (8u * k);
+            if (t < kTiles) {
+                const uint32_t tx = t % (kLaneBlock / 8u), ty = t / (kLaneBlock / 8u);
+                const uint32_t col = BX * kLbX + tx / kTilesX, row = BY * kLbY + ty;
+                if (col < gx && row < gy) cost[(row * gx + col) * kWavesPerTileGroup + tx % kTilesX] = sorted[t];
             }
-            out[t] = w;
         }
         return;
     }
-    uint32_t key = (c << 8) | t;
+    uint32_t key = (c << kLaneShift) | t;
     for (uint32_t size = 2; size <= 64u; size <<= 1) {
         for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
             const uint32_t other = (uint32_t)__shfl_xor((int)key, (int)stride, 64);
@@ -1728,23 +1739,25 @@ __global__ __launch_bounds__(256) void perm_kernel(const uint32_t* __restrict__ 
     sorted[t] = key;                // lane i of wave w: the wave's i-th largest key
     __syncthreads();
     uint32_t rank = lane;
-    for (uint32_t o = 1; o < 4u; ++o) {
-        const uint32_t* s = sorted + (((wave + o) & 3u) << 6);
-        uint32_t lo = 0, hi = 64;   // the number of s's keys above key (s descending)
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s[mid] > key) lo = mid + 1u;
-            else hi = mid;
-        }
-        rank += lo;
+#pragma unroll
+    for (uint32_t o = 1; o < kWaves; ++o) {
+        const uint32_t* s = sorted + (((wave + o) % kWaves) << 6);
+        uint32_t lo = 0;            // the number of s's keys above key (s descending)
+#pragma unroll
+        for (uint32_t step = 32; step > 0; step >>= 1)
+            if (s[lo + step - 1u] > key) lo += step;
+        rank += lo + (s[63] > key ? 1u : 0u);     // (all 64 above: lo stops at 63)
     }
-    reinterpret_cast<uint8_t*>(bytes)[rank] = (uint8_t)(key & 0xFFu);
+    slots[rank] = (PermT)(key & (kLanePixels - 1u));
     if (cost && (rank & 63u) == 0u) {
-        const uint32_t q = rank >> 6;
-        cost[((2u * B + (q >> 1)) * gx + bx) * kWavesPerTileGroup + (q & 1u)] = key >> 8;
+        const uint32_t q = rank >> 6, g = q / kTilesX;
+        const uint32_t col = BX * kLbX + g % kLbX, row = BY * kLbY + g / kLbX;
+        cost[(row * gx + col) * kWavesPerTileGroup + q % kTilesX] = key >> kLaneShift;
     }
     __syncthreads();
-    if (t < 64u) out[t] = bytes[t];
+    constexpr uint32_t kWords = kLanePixels * sizeof(PermT) / 4u;
+    uint32_t* out = reinterpret_cast<uint32_t*>(perm + (size_t)blockIdx.x * kLanePixels * sizeof(PermT));
+    if (t < kWords) out[t] = reinterpret_cast<const uint32_t*>(slots)[t];
 }
 
 // Heaviest tiles first: a counting sort of the tile groups by the cost an earlier
@@ -1980,11 +1993,15 @@ void march_grid(const KView& v, uint32_t& columns, uint32_t& rows) {
     rows = (v.local_rows + 8u * kTilesY - 1u) / (8u * kTilesY);
 }
 
+size_t perm_bytes(uint32_t gx, uint32_t gy) {
+    return (size_t)((gx + kLbX - 1u) / kLbX) * ((gy + kLbY - 1u) / kLbY) * kLanePixels * sizeof(PermT);
+}
+
 hipError_t launch_perm(const uint32_t* pcost, uint32_t LW, uint32_t rows, uint32_t gx, uint32_t gy, uint8_t* perm,
                        uint32_t* cost, hipStream_t stream) {
-    const uint32_t nb = gx * ((gy + 1u) / 2u);
+    const uint32_t nb = ((gx + kLbX - 1u) / kLbX) * ((gy + kLbY - 1u) / kLbY);
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(perm_kernel, dim3(nb), dim3(256), 0, stream, pcost, LW, rows, gx, gy, perm, cost);
+    hipLaunchKernelGGL(perm_kernel, dim3(nb), dim3(kLanePixels), 0, stream, pcost, LW, rows, gx, gy, perm, cost);
     return hipGetLastError();
 }
 
