@@ -316,6 +316,14 @@ __device__ __forceinline__ void lane_pixel(const KView& v, uint32_t& x, uint32_t
     }
 }
 
+// The tile pass's pixels by thread, (l << 16 | x), written once by march_kernel: a deferral
+// deep in the walk reads its pixel back with one LDS load instead of keeping it live or
+// recomputing it from the work and lane orders (two dependent global loads).
+__device__ __forceinline__ uint32_t* tile_pixels() {
+    __shared__ uint32_t p[64u * kTilesX * kTilesY];
+    return p;
+}
+
 // CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
 // crawling ray reserves an entry in the launch's deferral list and unwinds.
 // kExact (the crawl pass): every walk runs to its end here, and a loop round that
@@ -683,12 +691,8 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                         if (idx < v.defer_cap) {
                             // (the tile pass writes this pixel as 0; the crawl pass,
                             // which runs after it, overwrites it and counts its bytes)
-                            // (the pixel again from the workgroup's tile group and the lane
-                            // order: not kept live through the walk)
-                            uint32_t px_, pl_;
-                            lane_pixel(v, px_, pl_);
                             uint32_t* r = v.defer + 4 + (size_t)idx * kDeferRecWords;
-                            r[0] = (pl_ << 16) | px_;
+                            r[0] = tile_pixels()[threadIdx.x];   // (l << 16 | x), from LDS: not kept live through the walk
                             r[1] = (SHADOW ? 1u : 0u) | this->ctx;
                             r[2] = __float_as_uint(o.x); r[3] = __float_as_uint(o.y); r[4] = __float_as_uint(o.z);
                             r[5] = (uint32_t)cr.x; r[6] = (uint32_t)cr.y; r[7] = (uint32_t)cr.z;
@@ -1523,15 +1527,15 @@ __device__ __forceinline__ uint32_t light_and_shadow(Walker<STORE, COUNT, CRAWL>
     return lit * (uint32_t)!sh;
 }
 
-// Tile pass: hand pixel (x, local row l) to the crawl pass, to be walked there
+// Tile pass: hand this lane's pixel (tile_pixels) to the crawl pass, to be walked there
 // from its start (a record with flag 4).  Returns what the tile pass writes for
 // it: 0, or kDeferMarker when the list is full (the crawl pass then finds the
 // pixel by the marker).
-__device__ __forceinline__ uint32_t defer_rewalk(const KView& v, uint32_t x, uint32_t l) {
+__device__ __forceinline__ uint32_t defer_rewalk(const KView& v) {
     const uint32_t idx = atomicAdd(v.defer, 1u);
     if (idx < v.defer_cap) {
         uint32_t* r = v.defer + 4 + (size_t)idx * kDeferRecWords;
-        r[0] = (l << 16) | x;
+        r[0] = tile_pixels()[threadIdx.x];
         r[1] = 4u;
         return 0u;
     }
@@ -1582,7 +1586,7 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
                 bytes = 4u;
             } else {
                 bytes = 0u;
-                if (w.iters != kDeferredIters) col = defer_rewalk(v, x, l);
+                if (w.iters != kDeferredIters) col = defer_rewalk(v);
             }
         }
     }
@@ -1674,12 +1678,19 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, (TileWaves<ALGO, HI>::value
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t x, l;
     lane_pixel(v, x, l);
+    tile_pixels()[threadIdx.x] = (l << 16) | x;     // (read back only by this lane: no barrier)
     uint32_t bytes = 0, iters = 0;
     if (x < v.LW && l < v.local_rows) {
         // (&iters unconditionally: a pointer chosen by `v.cost ? &iters : nullptr` keeps
         // iters in scratch -- a store and a reload per lane, 8 MB of WRITE_SIZE per C2 launch)
-        v.out[(size_t)l * v.LW + x] = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes, &iters);
-        if (v.pcost) v.pcost[(size_t)l * v.LW + x] = iters;    // the pixel's walk length, for the next lane order
+        const uint32_t c = shade<STORE, ALGO, COUNT, false>(s, v, x, l, bytes, &iters);
+        // (x and l again from LDS, so they are not live through the walk; the empty asm
+        // keeps the compiler from forwarding the stored value instead)
+        asm volatile("" ::: "memory");
+        const uint32_t p = tile_pixels()[threadIdx.x];
+        const size_t at = (size_t)(p >> 16) * v.LW + (p & 0xFFFFu);
+        v.out[at] = c;
+        if (v.pcost) v.pcost[at] = iters;         // the pixel's walk length, for the next lane order
     }
     if (COUNT) add_bytes(v, lane, bytes);
     if (v.cost) {                                  // the wave's walk length, for the next work order
