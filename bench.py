@@ -22,16 +22,18 @@ k's gather runs beside frame k+1's render.  Every frame is still rendered in ful
 Inputs (scene, camera) are resident in HBM before timing starts; the timed region
 ends after the last frame's gather and assembly.  Rank 0 prints ONE JSON line.
 
-`value`/`ms_per_step` are the pipelined throughput; `kernel_ms` (learned work order)
-and `kernel_ms_grid_order` (a first render's grid order) are one launch timed alone:
-one pair of HIP events around 200 isolated launches on the launch stream.
+`value`/`ms_per_step` are the pipelined throughput; `kernel_ms_first_render` (nothing
+learned: grid order, 8x8 tiles), `kernel_ms_grid_order` (grid order, the lane order learned
+from earlier launches of the view) and `kernel_ms` (both learned orders) are one launch
+timed alone: one pair of HIP events around 200 isolated launches on the launch stream.
 
-roofline: `achieved`/`frac` are the north star's figure for ONE launch in grid order --
-the algorithmic bytes the launch issues (the words the reference walk
+roofline: `achieved`/`frac` are the north star's figure for ONE launch as a first render
+-- the algorithmic bytes the launch issues (the words the reference walk
 reads, counted by the instrumented kernel, minus the existence reads of the crawl
 iterations the crawl pass fast-forwards in closed form and never loads:
 `algorithmic_bytes_issued_per_launch`, `crawl_iterations_fast_forwarded`) /
-`kernel_ms_grid_order` / 8 TB/s.  `frac_learned_order` uses `kernel_ms`,
+`kernel_ms_first_render` / 8 TB/s.  `frac_grid_order` uses `kernel_ms_grid_order`,
+`frac_learned_order` `kernel_ms`,
 `frac_pipelined` `ms_per_step` (C2 reaches ~1.0 there: its counted 4-B words are
 answered by 8-B mask-record loads that mostly hit the vector L1 -- DESIGN.md 6),
 `frac_section8d` the unreduced 8(d) bytes.  `dispatch_phases` lists the run's
@@ -316,6 +318,15 @@ def main():
     # kernel_ms = phase time / n_iso -- each launch's tile and crawl passes plus the
     # dispatch gaps between back-to-back launches on one stream.
     n_iso = max(args.steps, 200)
+    # A first render of the view, n_iso times: what the device learned (work and lane orders,
+    # include/vr.h vr_forget_orders) is dropped before every launch, so each one renders as
+    # the reference's one-frame CLI run does (Main.cu:105-163) -- grid order, 8x8 tiles
+    ev_first = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev_first[0].record(stream)
+    for _ in range(n_iso):
+        vr.forget_orders(dev.index)
+        render(pipe.bufs[0])
+    ev_first[1].record(stream)
     for _ in range(40):
         render(pipe.bufs[0])
 
@@ -366,6 +377,7 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     kern_ms = ev[0].elapsed_time(ev[1]) / n_iso
     kern_grid_ms = ev_grid[0].elapsed_time(ev_grid[1]) / n_iso
+    kern_first_ms = ev_first[0].elapsed_time(ev_first[1]) / n_iso
     mrays = W * H / (ms_per_step * 1e-3) / 1e6
     if args.dump_frame and rank == 0:
         np.save(args.dump_frame, pipe.last_frame().cpu().numpy())
@@ -375,12 +387,12 @@ def main():
             return nbytes / (ms * 1e-3) / 1e9
         # The roofline's numerator: the bytes this launch's walks stand for minus
         # the existence reads of crawl iterations the crawl pass fast-forwards in closed form
-        # (it never issues them).  Its duration: one launch on its own, in grid order -- a
-        # first render, as the reference's CLI makes (Main.cu:105-163), with no work order
-        # learned from earlier launches of the view.  (With frames in flight a launch's
-        # events also span the other frame's work, so no per-launch duration exists there;
-        # the pipelined rate is frac_pipelined.)
-        achieved = gbs(issued_bytes, kern_grid_ms)
+        # (it never issues them).  Its duration: one launch on its own as a first render, as
+        # the reference's CLI makes (Main.cu:105-163), with no work or lane order learned from
+        # earlier launches of the view.  (With frames in flight a launch's events also span
+        # the other frame's work, so no per-launch duration exists there; the pipelined rate
+        # is frac_pipelined.)
+        achieved = gbs(issued_bytes, kern_first_ms)
         tj = load_traffic(args.traffic_json, cfg.name, world)
         traffic = tj.get("hbm_bytes_per_launch")
         roof = {"bound": None, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -388,20 +400,23 @@ def main():
                 "achieved_basis": "algorithmic bytes issued per launch (SURVEY 8(d): the words the reference walk "
                                   "reads, counted by the instrumented kernel, minus the existence reads of crawl "
                                   "iterations fast-forwarded in closed form) / the mean duration of one launch "
-                                  "alone in grid order (kernel_ms_grid_order: tile pass + crawl pass, one HIP event "
-                                  "pair on the launch stream around the phase's back-to-back launches) -- mostly "
-                                  "served from L2/MALL, not HBM",
+                                  "alone as a first render (kernel_ms_first_render: learned orders dropped before "
+                                  "every launch; tile pass + crawl pass, one HIP event pair on the launch stream "
+                                  "around the phase's back-to-back launches) -- mostly served from L2/MALL, not HBM",
                 "algorithmic_bytes_per_launch": launch_bytes,
                 "algorithmic_bytes_issued_per_launch": issued_bytes,
                 "crawl_iterations_fast_forwarded": ff_iters,
                 "algorithmic_bytes_per_frame": frame_bytes, "algorithmic_bytes_issued_per_frame": frame_issued,
+                "frac_grid_order": round(gbs(issued_bytes, kern_grid_ms) / HBM_PEAK_GBS, 4),
                 "frac_learned_order": round(gbs(issued_bytes, kern_ms) / HBM_PEAK_GBS, 4),
                 "frac_pipelined": round(gbs(issued_bytes, ms_per_step) / HBM_PEAK_GBS, 4),
-                "frac_section8d": round(gbs(launch_bytes, kern_grid_ms) / HBM_PEAK_GBS, 4),
-                "fracs_basis": "the same issued bytes over kernel_ms (one launch alone, heaviest tile groups first "
-                               "from an earlier launch's costs) and over ms_per_step (the pipelined frame rate); "
-                               "frac_section8d: the full SURVEY 8(d) count over kernel_ms_grid_order (crawl "
-                               "iterations credited as if loaded). profiles/roofline_phases.py recomputes frac and "
+                "frac_section8d": round(gbs(launch_bytes, kern_first_ms) / HBM_PEAK_GBS, 4),
+                "fracs_basis": "the same issued bytes over kernel_ms_grid_order (one launch alone in grid order "
+                               "with the lane order learned from earlier launches of the view), kernel_ms (one "
+                               "launch alone, heaviest tile groups first as well) and ms_per_step (the pipelined "
+                               "frame rate); frac_section8d: the full SURVEY 8(d) count over "
+                               "kernel_ms_first_render (crawl iterations credited as if loaded). "
+                               "profiles/roofline_phases.py recomputes frac, frac_grid_order and "
                                "frac_learned_order from a rocprofv3 kernel trace of the same run",
                 }
         hbm_frac = valu_frac = None
@@ -469,16 +484,20 @@ def main():
                        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default")},
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_grid_order": round(kern_grid_ms, 4),
+            "kernel_ms_first_render": round(kern_first_ms, 4),
             "kernel_ms_basis": f"{n_iso} launches one after the other on one stream, one HIP event pair around them "
                                "(each: tile pass + crawl pass): kernel_ms with the AUTO schedule (heaviest tile "
-                               "groups first, learned from earlier launches of the same view), kernel_ms_grid_order "
-                               "in grid order (a first render)",
-            "kernel_mrays_per_s": round(W * H / world / (kern_grid_ms * 1e-3) / 1e6, 2),
+                               "groups first and the lane order, both learned from earlier launches of the same "
+                               "view), kernel_ms_grid_order in grid order with the learned lane order, "
+                               "kernel_ms_first_render with what the device learned dropped before every launch "
+                               "(vr_forget_orders: grid order, 8x8 tiles -- a first render)",
+            "kernel_mrays_per_s": round(W * H / world / (kern_first_ms * 1e-3) / 1e6, 2),
             "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "roofline": roof,
             # the non-instrumented launches of this run in order, per phase (a rocprofv3 kernel
             # trace of the same command splits into them: profiles/roofline_phases.py)
-            "dispatch_phases": {"warmup": args.warmup, "untimed": 40, "iso_grid": n_iso, "iso_learned": n_iso,
+            "dispatch_phases": {"warmup": args.warmup, "iso_first": n_iso, "untimed": 40, "iso_grid": n_iso,
+                                "iso_learned": n_iso,
                                 "latency": 5 if grouped else 0, "timed": args.steps},
         }
         if HW_QUEUES_REQUESTED is not None:

@@ -31,5 +31,6 @@ for rnd in range(int(opts["--rounds"])):
         d = json.loads(js[-1])
         ro = d["roofline"]
         print(f"[{rnd}] {os.path.basename(lib)}{':' + extra if extra else ''}: {cfg} ms/step {d['ms_per_step']:.4f} "
-              f"kernel_ms {d['kernel_ms']:.4f} grid {d['kernel_ms_grid_order']:.4f} frac {ro['frac']:.3f} "
+              f"kernel_ms {d['kernel_ms']:.4f} grid {d['kernel_ms_grid_order']:.4f} "
+              f"first {d.get('kernel_ms_first_render', 0):.4f} frac {ro['frac']:.3f} "
               f"learned {ro['frac_learned_order']:.3f} bytes {ro['algorithmic_bytes_per_launch']}", flush=True)

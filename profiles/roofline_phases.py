@@ -5,10 +5,10 @@ recompute every roofline fraction of its JSON line from the trace alone.
   python profiles/roofline_phases.py <run_kernel_trace.csv> <bench_line.json> [out_dir]
 
 bench.py prints `dispatch_phases` -- the number of non-instrumented launches per phase, in
-submission order: warmup, untimed, iso_grid, iso_learned, latency (N > 1), timed.  Every
-launch is one tile-pass dispatch (`march_kernel<S, A, false[, HI]>`) followed by one crawl-pass
-dispatch (`crawl_kernel<S, A, false>`) on the same stream, sometimes plus a work-order build
-(`order_kernel`, every 16th heaviest-first launch of a slot).  Dispatches are taken in
+submission order: warmup, iso_first, untimed, iso_grid, iso_learned, latency (N > 1), timed.
+Every launch is one tile-pass dispatch (`march_kernel<S, A, false[, HI]>`) followed by one
+crawl-pass dispatch (`crawl_kernel<S, A, false>`) on the same stream, sometimes plus the
+learned orders' builds (`perm_kernel`, `order_kernel`: about every 16th launch of a slot).  Dispatches are taken in
 Dispatch_Id order (submission order); the instrumented launch (`<..., true>`) is not counted.
 
 For each phase it writes `kernel_stats_<phase>.csv` (rocprofv3's kernel_stats.csv columns,
@@ -18,8 +18,9 @@ over that phase's dispatches only) and reports
   kernels = the sum of the phase's per-kernel mean durations (tile + crawl + order builds
             per launch): the kernel_stats figure, without the dispatch gaps,
 and the fraction algorithmic_bytes_issued_per_launch / duration / 8 TB/s for both, next
-to the bench's own figure for that phase: frac (iso_grid: one launch alone, grid order),
-frac_learned_order (iso_learned) and frac_pipelined (timed: per frame).
+to the bench's own figure for that phase: frac (iso_first: one launch alone as a first
+render), frac_grid_order (iso_grid: grid order, learned lane order), frac_learned_order
+(iso_learned) and frac_pipelined (timed: per frame).
 Results: <out_dir>/roofline_phases.json.
 """
 from __future__ import annotations
@@ -56,7 +57,7 @@ def main():
         if "vr::" not in name:
             continue
         kind = ("tile" if "march_kernel" in name else "crawl" if "crawl_kernel" in name else
-                "order" if "order_kernel" in name else None)
+                "order" if ("order_kernel" in name or "perm_kernel" in name) else None)
         if kind is None or re.search(r"kernel<\d+, \d+, true[,>]", name):
             continue
         rows.append((int(r["Dispatch_Id"]), kind, name, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
@@ -112,7 +113,8 @@ def main():
             "frac_from_trace": frac(period_ns),
             "frac_from_kernel_means": frac(kern_ns),
         }
-    bench = {"iso_grid": roof.get("frac"), "iso_learned": roof.get("frac_learned_order"),
+    bench = {"iso_first": roof.get("frac"), "iso_grid": roof.get("frac_grid_order"),
+             "iso_learned": roof.get("frac_learned_order"),
              "timed": roof.get("frac_pipelined")}
     for ph, fb in bench.items():
         if ph in res["phases"] and fb:

@@ -157,6 +157,15 @@ def test_band_buffer_words():
     assert vr.band_buffer_words(10, 10, 0, 3) == 0
 
 
+def test_forget_orders_checks_device_index():
+    # host bookkeeping only (no HIP call): valid indices succeed with or without a GPU
+    vr.forget_orders(0)
+    vr.forget_orders(63)
+    for bad in (-1, 64):
+        with pytest.raises(vr.VrError):
+            vr.forget_orders(bad)
+
+
 def test_assemble_bands_cpu():
     from voxelraymarcher_amd.tiles import assemble_bands, owned_rows
     W, H, B = 7, 29, 4

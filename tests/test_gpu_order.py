@@ -45,7 +45,8 @@ def test_ordered_launches_two_views_in_flight(algo):
     img = refs[0].cpu().numpy().view(np.uint32)
     assert hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest() == FRAMES[name]["sha256"]
     # 48 launches (three uses of each of the ring's 16 slots) on two streams, the two views
-    # alternating in runs of three so that orders made for one view serve the other
+    # alternating in runs of three: each view's orders are learned within its runs (a launch
+    # whose previous launch rendered the same view) and used only for that view
     streams = [torch.cuda.Stream() for _ in range(2)]
     for s in streams:
         s.wait_stream(torch.cuda.current_stream())
@@ -132,4 +133,38 @@ def test_lane_order_ragged_frames(store):
                 if ref is None:
                     ref = out.clone()
                 assert torch.equal(out, ref), (store, W, H, algo.name, i)
+    scene.close()
+
+
+def test_forget_orders_first_render_and_view_keys():
+    # vr_forget_orders drops what the device learned: the next launch is a first render; the
+    # orders come back after repeated launches of the view and are never used for another view
+    # of the same grid size -- every frame stays the oracle's
+    cfg = vr.CONFIGS["C2"]
+    xyz, rgb = cfg.voxels()
+    scene = vr.create_scene(xyz, rgb, cfg.store)
+    W, H = cfg.width, cfg.height
+    lit = vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    cams = [vr.Camera.reference(W, H),
+            vr.Camera((-3.0, 5.0, 8.0), (1.0, -1.0, -2.0), (0.0, 1.0, 0.0), 50.0, W / H)]
+    out = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
+    refs = []
+    for cam in cams:
+        vr.forget_orders(0)
+        out.fill_(-1)
+        vr.run_raymarching_kernel(scene, vr.RayMarchAlgorithm.ORIGINAL, cam, lit, info, W, H, out)
+        torch.cuda.synchronize()
+        refs.append(out.clone())
+    img = refs[0].cpu().numpy().view(np.uint32)
+    assert hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest() == FRAMES["C2"]["sha256"]
+    seq = [0] * 40 + [1] * 3 + [0] * 20 + ["forget", 0, 0] + [1, 0] * 10
+    for i, k in enumerate(seq):
+        if k == "forget":
+            vr.forget_orders(0)
+            continue
+        out.fill_(-1)
+        vr.run_raymarching_kernel(scene, vr.RayMarchAlgorithm.ORIGINAL, cams[k], lit, info, W, H, out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, refs[k]), (i, k)
     scene.close()

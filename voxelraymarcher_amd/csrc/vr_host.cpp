@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -557,6 +558,7 @@ struct SlotRing {
             uint32_t* cost = nullptr;      // kWavesPerTileGroup words per tile group
             uint32_t* order = nullptr;     // one word per tile group
             uint32_t cap = 0, gx = 0, gy = 0, age = 0;
+            uint64_t key = 0;              // the view it was learned on (view_key)
             bool valid = false;
             // the lane order (vr_march.hip lane_pixel): per-pixel walk lengths and, per 16x16
             // block, its pixels heaviest first, for a grid of lgx x lgy
@@ -564,6 +566,7 @@ struct SlotRing {
             uint8_t* perm = nullptr;       // vr::perm_bytes(lgx, lgy)
             size_t pcap = 0, bcap = 0;
             uint32_t lgx = 0, lgy = 0, lage = 0;
+            uint64_t lkey = 0;
             bool lvalid = false;
             bool relaned = false;          // the lane order changed after the work order's costs
         };
@@ -571,6 +574,7 @@ struct SlotRing {
         bool any = false;                  // the device's previous launch: its stream and slot
         hipStream_t last_stream = nullptr;
         uint32_t last_idx = 0;
+        uint64_t last_key = 0;             // the view of the device's previous launch
     } dev[64];
     SlotRing(const char* n, size_t w, uint32_t s) : name(n), words(w), nslots(s) {}
 };
@@ -697,6 +701,24 @@ bool order_enabled() {
     return on;
 }
 
+// The view a launch renders, for the learned orders: an FNV-1a hash of the scene, the
+// algorithm and every value field of the view (camera, lights, transform, frame size, the
+// launch's rows and its band / tile deal; make_view zeroes the struct, so its padding is 0).
+// The per-launch buffers (out and after) are not part of it.
+uint64_t view_key(const vr_scene* s, vr_algo algo, const vr::KView& v) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+        const unsigned char* b = (const unsigned char*)p;
+        for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    };
+    const uintptr_t sp = (uintptr_t)s;
+    const uint32_t a = (uint32_t)algo;
+    mix(&sp, sizeof sp);
+    mix(&a, sizeof a);
+    mix(&v, offsetof(vr::KView, out));
+    return h;
+}
+
 int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, uint32_t occupancy, vr::KView& v,
            void* stream) {
     if (algo != VR_ALGO_ORIGINAL && algo != VR_ALGO_LONGESTAXIS) return fail(VR_E_INVALID, "unknown algorithm");
@@ -747,6 +769,14 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     D.any = true;
     D.last_stream = st;
     D.last_idx = lease.idx;
+    // Orders are learned per view: one made for another view (e.g. the previous rank of a
+    // one-GPU rank emulation, or a moved camera) would deal the wrong pixels together.  A
+    // view whose previous launch on the device was the same view gets its orders made (on
+    // each slot's first such launch); a view that changes every launch never does, and
+    // renders as a first render does.
+    const uint64_t key = view_key(s, algo, v);
+    const bool repeat = D.last_key == key;
+    D.last_key = key;
     if (heavy && order_enabled() && n != 0) {
         if (n > O.cap) {
             // Grow, stream-ordered: the slot's previous launch -- the last user of the old
@@ -769,11 +799,11 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
             }
             O.cap = n;
         }
-        const bool match = O.valid && O.gx == gx && O.gy == gy;
+        const bool match = O.valid && O.gx == gx && O.gy == gy && O.key == key;
         v.order = match ? O.order : nullptr;
         // (a work order made from costs walked under another lane order is remade: the lane
         // order moves the heavy pixels of a block into one of its two tile groups)
-        remake = !match || O.relaned || ++O.age >= order_refresh();
+        remake = match ? (O.relaned || ++O.age >= order_refresh()) : repeat;
         v.cost = remake ? O.cost : nullptr;
     }
     // The lane order, kept like the work order but for every schedule: this slot's if it was
@@ -806,9 +836,9 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
             O.pcap = npx;
             O.bcap = nperm;
         }
-        const bool match = O.lvalid && O.lgx == gx && O.lgy == gy;
+        const bool match = O.lvalid && O.lgx == gx && O.lgy == gy && O.lkey == key;
         v.perm = match ? O.perm : nullptr;
-        relane = !match || ++O.lage >= order_refresh();
+        relane = match ? ++O.lage >= order_refresh() : repeat;
         v.pcost = relane ? O.pcost : nullptr;
     }
     // crawl pass grid from the records an earlier launch deferred (a hint: any grid renders
@@ -833,6 +863,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         O.relaned = !with_costs;
         O.lgx = gx;
         O.lgy = gy;
+        O.lkey = key;
         O.lage = 0;
     }
     if (e == hipSuccess && (remake || with_costs)) {
@@ -857,6 +888,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         O.valid = e == hipSuccess;
         O.gx = gx;
         O.gy = gy;
+        O.key = key;
         O.age = 0;
         O.relaned = false;
     }
@@ -1243,6 +1275,15 @@ uint64_t vr_band_buffer_words(uint32_t width, uint32_t height, uint32_t band_row
 
 uint32_t vr_deal_stride_default(uint32_t nranks) {
     return (nranks % 3u == 0u) ? 1u : 3u;
+}
+
+int vr_forget_orders(int device) {
+    if (device < 0 || device >= 64) return fail(VR_E_INVALID, "device index out of range");
+    SlotRing::Dev& D = g_defer_ring.dev[device];
+    std::lock_guard<std::mutex> lk(D.mu);
+    for (SlotRing::Dev::Order& O : D.ord) O.valid = O.lvalid = O.relaned = false;   // (buffers kept)
+    D.last_key = 0;
+    return VR_OK;
 }
 
 uint64_t vr_tile_buffer_words(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t tile_cols, uint32_t nranks) {

@@ -371,6 +371,12 @@ def deal_stride_default(nranks: int) -> int:
     return int(lib().vr_deal_stride_default(nranks))
 
 
+def forget_orders(device: int = 0) -> None:
+    """Drop the work and lane orders the device learned (vr_forget_orders): the next launch
+    renders as a first render of its view."""
+    check(lib().vr_forget_orders(int(device)), "vr_forget_orders")
+
+
 def render_tiles(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
                  info: VoxelSceneInfo, width: int, height: int, band_rows: int, tile_cols: int, rank: int,
                  nranks: int, out: torch.Tensor, stream=None) -> torch.Tensor:
