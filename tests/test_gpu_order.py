@@ -64,7 +64,8 @@ def test_ordered_launches_two_views_in_flight(algo):
 
 
 def test_ordered_launches_grid_change():
-    # orders are per grid size: alternating frame sizes never use an order of the other size
+    # orders are per view: frame sizes alternating in runs of two (each view's orders made on
+    # its repeats) never use an order of another size
     cfg = vr.CONFIGS["C1"]
     xyz, rgb = cfg.voxels()
     scene = vr.create_scene(xyz, rgb, cfg.store)
@@ -78,8 +79,8 @@ def test_ordered_launches_grid_change():
                                   out)
         torch.cuda.synchronize()
         refs[(W, H)] = out.clone()
-    for i in range(60):
-        W, H = sizes[i % 3]
+    for i in range(96):
+        W, H = sizes[(i // 2) % 3]
         out = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
         vr.run_raymarching_kernel(scene, vr.RayMarchAlgorithm.ORIGINAL, vr.Camera.reference(W, H), lit, info, W, H,
                                   out)

@@ -131,7 +131,11 @@ struct DevBuf {
 
 }  // namespace
 
+std::atomic<uint64_t> g_scene_serial{0};
 struct vr_scene {
+    // a process-unique id (the learned orders' view key: a later scene may reuse a freed
+    // scene's address)
+    const uint64_t serial = ++g_scene_serial;
     int device = 0;
     vr_store store = VR_STORE_VCS;
     uint32_t D = 1;
@@ -657,17 +661,19 @@ struct SlotLease {
     }
 };
 
-// Heaviest-first work order: remade every VR_ORDER_REFRESH (16) launches of
-// a slot (16 slots: about one order build per 16 launches of a device).  VR_ORDER=0 turns
-// it off.
+// Heaviest-first work order and lane order: made once per slot and view -- a
+// view's walk lengths do not change (scenes are immutable), so they are not remade unless
+// VR_ORDER_REFRESH=N (experiments) asks for a remake every N uses of a slot.  VR_ORDER=0 /
+// VR_LANE_ORDER=0 turn them off.
 uint32_t order_refresh() {
     static const uint32_t r = [] {
         const char* e = std::getenv("VR_ORDER_REFRESH");
-        const long v = e ? std::strtol(e, nullptr, 10) : 16;
-        return (uint32_t)(v >= 1 ? v : 16);
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (uint32_t)(v >= 1 ? v : 0);
     }();
     return r;
 }
+bool refresh_due(uint32_t& age) { return order_refresh() != 0 && ++age >= order_refresh(); }
 // VR_CRAWL_RPW (A/B runs): crawl records per wave for every launch instead of 4 / 8.
 uint32_t crawl_rpw_override() {
     static const uint32_t r = [] {
@@ -711,9 +717,8 @@ uint64_t view_key(const vr_scene* s, vr_algo algo, const vr::KView& v) {
         const unsigned char* b = (const unsigned char*)p;
         for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
     };
-    const uintptr_t sp = (uintptr_t)s;
     const uint32_t a = (uint32_t)algo;
-    mix(&sp, sizeof sp);
+    mix(&s->serial, sizeof s->serial);
     mix(&a, sizeof a);
     mix(&v, offsetof(vr::KView, out));
     return h;
@@ -748,10 +753,9 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     v.defer_cap = (v.defer_cap && v.defer_cap < vr::kDeferCap) ? v.defer_cap : vr::kDeferCap;
     v.defer_stat = lease.D().stat_dev;
     const uint32_t expect = *(volatile uint32_t*)lease.D().stat_host;   // an earlier launch's count (a hint)
-    // The work order: this slot's order if it was made for this grid, remade (from this
-    // launch's costs, after its passes) when missing or every order_refresh() uses of the slot.
-    // It only permutes the tile groups; a view of the same grid size that it was not made
-    // for renders the same pixels, just in a worse order.
+    // The work order: this slot's order if it was made for this view, made (from this
+    // launch's costs, after its passes) when missing and the view repeats.  It only permutes
+    // the tile groups: any order renders the same pixels.
     uint32_t gx = 0, gy = 0;
     vr::march_grid(v, gx, gy);
     const uint32_t n = gx * gy;
@@ -788,13 +792,17 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
                 const hipError_t e2 = hipFreeAsync(O.order, st);
                 if (e == hipSuccess) e = e2;
             }
-            O = SlotRing::Dev::Order{};
+            O.cost = nullptr;        // (the work order's fields only: the lane order's are its own)
+            O.order = nullptr;
+            O.cap = 0;
+            O.valid = false;
             if (e == hipSuccess) e = hipMallocAsync((void**)&O.cost, sizeof(uint32_t) * vr::kWavesPerTileGroup * (size_t)n, st);
             if (e == hipSuccess) e = hipMallocAsync((void**)&O.order, sizeof(uint32_t) * (size_t)n, st);
             if (e != hipSuccess) {
                 if (O.cost) (void)hipFreeAsync(O.cost, st);
                 if (O.order) (void)hipFreeAsync(O.order, st);
-                O = SlotRing::Dev::Order{};
+                O.cost = nullptr;
+                O.order = nullptr;
                 return hip_fail(e, "work order buffers");
             }
             O.cap = n;
@@ -803,13 +811,13 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         v.order = match ? O.order : nullptr;
         // (a work order made from costs walked under another lane order is remade: the lane
         // order moves the heavy pixels of a block into one of its two tile groups)
-        remake = match ? (O.relaned || ++O.age >= order_refresh()) : repeat;
+        remake = match ? (O.relaned || refresh_due(O.age)) : repeat;
         v.cost = remake ? O.cost : nullptr;
     }
     // The lane order, kept like the work order but for every schedule: this slot's if it was
-    // made for this grid, remade from this launch's per-pixel walk lengths when missing or
-    // every order_refresh() uses.  It permutes pixels within 16x16 blocks only, so any view
-    // of the same grid renders the same pixels with it.
+    // made for this view, made from this launch's per-pixel walk lengths when missing and the
+    // view repeats.  It permutes pixels within 16x16 blocks only: any permutation renders the
+    // same pixels.
     bool relane = false;
     const size_t npx = (size_t)v.LW * v.local_rows, nperm = vr::perm_bytes(gx, gy);
     if (lane_order_enabled() && n != 0) {
@@ -838,7 +846,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         }
         const bool match = O.lvalid && O.lgx == gx && O.lgy == gy && O.lkey == key;
         v.perm = match ? O.perm : nullptr;
-        relane = match ? ++O.lage >= order_refresh() : repeat;
+        relane = match ? refresh_due(O.lage) : repeat;
         v.pcost = relane ? O.pcost : nullptr;
     }
     // crawl pass grid from the records an earlier launch deferred (a hint: any grid renders
