@@ -7,7 +7,7 @@ roofline of the dominant kernel and the CPU oracle baseline.
                   [--tiling auto|weak|fixed]
 
 A step = one full frame.  With N > 1 ranks the frame is dealt over the ranks --
-fixed tiling: the 2-D tile deal (every 8-row band cut into 16-column blocks, block j
+fixed tiling: the 2-D tile deal (every 16-row band cut into 16-column blocks, block j
 of band b -> rank (j + 3b) % N, so expensive rows are spread over every rank; --layout
 bands keeps whole 8-row bands, band b -> rank b % N); weak tiling: 8-row bands -- each
 rank renders its share and every frame is gathered to rank 0 over RCCL as RGB8 (3 B
@@ -91,7 +91,7 @@ def parse():
     p.add_argument("--resolution", default="",
                    help="WxH instead of the config's frame (tests; the same view and scene)")
     p.add_argument("--layout", default="auto", choices=["auto", "bands", "tiles"],
-                   help="how the frame is dealt over N > 1 ranks: 8-row bands, or the 2-D tile deal (8-row bands "
+                   help="how the frame is dealt over N > 1 ranks: 8-row bands, or the 2-D tile deal (16-row bands "
                         "cut into --tile-cols column blocks); auto = tiles for fixed tiling, bands for weak")
     p.add_argument("--tile-cols", type=int, default=16, help="column block of the 2-D tile deal (one workgroup)")
     p.add_argument("--exchange", action="store_true",
@@ -131,7 +131,9 @@ from voxelraymarcher_amd.tiles import BandGather, frame_resolution, init_frame_g
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 N_SIMD = 1024              # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles (SIMD-32)
-BAND_ROWS = 8              # one wave tile high
+BAND_ROWS = 8              # row bands: one wave tile high
+TILE_BAND_ROWS = 16        # 2-D tile deal: a 16x16 block per deal unit, one lane-order block
+                           # (8-row bands put two frame strips in one block: C5 rank 0.099 vs 0.089 ms)
 HEADLINE = "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s"   # BASELINE.json metric
 
 
@@ -273,15 +275,16 @@ def main():
     # pixel): rank 0 ends each frame with the RGB8 image
     depth = args.frames_in_flight or pipeline_depth(args.config)
     layout = args.layout if args.layout != "auto" else ("tiles" if tiling == "fixed" else "bands")
-    pipe = BandGather(W, H, BAND_ROWS, rank, world, dev, depth=depth, rgb8=grouped, stage_host=stage_host,
+    band_rows = TILE_BAND_ROWS if layout == "tiles" else BAND_ROWS
+    pipe = BandGather(W, H, band_rows, rank, world, dev, depth=depth, rgb8=grouped, stage_host=stage_host,
                       tile_cols=args.tile_cols if layout == "tiles" else 0, exchange=grouped)
     tcols = pipe.T          # 0: row bands (every N = 1 run without --exchange)
 
     def render(buf):   # on the current stream (BandGather's slot stream in the loops)
         if tcols:
-            vr.render_tiles(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, tcols, rank, world, buf)
+            vr.render_tiles(scene, cfg.algorithm, cam, lit, info, W, H, band_rows, tcols, rank, world, buf)
         else:
-            vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, BAND_ROWS, rank, world, buf)
+            vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, band_rows, rank, world, buf)
 
     # algorithmic bytes of THIS rank's launch (its bands; instrumented kernel,
     # untimed) and of the whole frame (sum over ranks); `stats`: the part of
@@ -289,7 +292,7 @@ def main():
     # (their existence reads are counted, never issued)
     ctr = torch.zeros(1, dtype=torch.int64, device=dev)
     stats = torch.zeros(2, dtype=torch.int64, device=dev)
-    vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, pipe.bufs[0], band_rows=BAND_ROWS, rank=rank,
+    vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, pipe.bufs[0], band_rows=band_rows, rank=rank,
                  nranks=world, counter=ctr, stats=stats, tile_cols=tcols)
     torch.cuda.synchronize()
     launch_bytes = int(ctr.item())
@@ -331,7 +334,7 @@ def main():
         render(pipe.bufs[0])
 
     def render_grid(buf):
-        vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=BAND_ROWS, rank=rank, nranks=world,
+        vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=band_rows, rank=rank, nranks=world,
                      stream=stream, schedule=vr.Schedule.GRID, tile_cols=tcols)
 
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -458,7 +461,7 @@ def main():
              f"achieved HBM GB/s")
         gather = ("RCCL gather" if backend == "nccl" else "gloo gather staged through host memory") + \
             (" (ranks sharing cuda:0)" if args.same_device else "")
-        deal = (f"2-D tile deal x{world} (8x{tcols} blocks, block j of 8-row band b -> rank (j + "
+        deal = (f"2-D tile deal x{world} ({band_rows}x{tcols} blocks, block j of {band_rows}-row band b -> rank (j + "
                 f"{pipe.stride}b) % {world})" if tcols else f"row-band tiles x{world}")
         par = deal + (f" + {gather} of the RGB8 tiles to rank 0 (overlapped with the next frame)" if grouped else "")
         line = {

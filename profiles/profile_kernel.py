@@ -24,6 +24,8 @@ p.add_argument("--no-shadows", action="store_true")
 p.add_argument("--algo", choices=["original", "longestaxis"], default=None)
 p.add_argument("--store", choices=["vcs", "hashtable"], default=None)
 p.add_argument("--kernel", choices=["auto", "tile", "rewalk"], default="auto")
+p.add_argument("--world", type=int, default=1, help="> 1: render only --rank's share of the 2-D tile deal")
+p.add_argument("--rank", type=int, default=0)
 a = p.parse_args()
 kern = {"auto": vr.Kernel.AUTO, "tile": vr.Kernel.TILE, "rewalk": vr.Kernel.TILE_REWALK}[a.kernel]
 cfg = vr.CONFIGS[a.config]
@@ -37,13 +39,22 @@ lit = vr.setup_constant_values(use_shadows=not a.no_shadows)
 info = vr.VoxelSceneInfo((0, 0, 0), cfg.scale)
 out = torch.empty(W * H, dtype=torch.int32, device="cuda")
 s = torch.cuda.current_stream()
+
+
+def render():
+    if a.world > 1:     # one rank's tiles (8-row bands, 16-column blocks), as bench.py's fixed tiling
+        vr.render_tiles(scene, algo, cam, lit, info, W, H, 8, 16, a.rank, a.world, out)
+    else:
+        vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, kernel=kern)
+
+
 for _ in range(1 + a.warmup):
-    vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, kernel=kern)
+    render()
 torch.cuda.synchronize()
 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
 for e0, e1 in ev:
     e0.record(s)
-    vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, kernel=kern)
+    render()
     e1.record(s)
 torch.cuda.synchronize()
 ms = [e0.elapsed_time(e1) for e0, e1 in ev]

@@ -35,6 +35,18 @@ print(f"pipelined: {steps} frames, span {(t1 - t0) / 1e3:.1f} us = {(t1 - t0) / 
 for kind in ("march", "crawl", "pack"):
     d = [e - s for s, e, n in pipe if short(n) == kind]
     print(f"  {kind:5s}: mean dispatch {sum(d) / len(d) / 1e3:8.2f} us (overlapping)")
+# what runs when: the pipelined span split by the set of kernel kinds active
+pts = sorted([(s_, 1, short(n)) for s_, _, n in pipe] + [(e_, -1, short(n)) for _, e_, n in pipe])
+act = {"march": 0, "crawl": 0, "pack": 0}
+mix = {}
+prev = pts[0][0]
+for t, d, k in pts:
+    state = "+".join(x for x in ("march", "crawl", "pack") if act[x]) or "idle"
+    mix[state] = mix.get(state, 0) + (t - prev)
+    prev = t
+    act[k] += d
+tot = sum(mix.values())
+print("  active kinds over the span: " + ", ".join(f"{k} {v / tot:.3f}" for k, v in sorted(mix.items(), key=lambda kv: -kv[1])))
 lo = ev[per * (warm + steps):]
 tm, tc, tp, gaps = [], [], [], []
 for i in range(0, len(lo), per):

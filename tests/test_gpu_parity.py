@@ -173,14 +173,15 @@ def test_c5_crawl_pixels_fixture(c5):
 def test_c5_eight_rank_emulation(c5, layout):
     """C5 as BASELINE defines it -- the fixed 3840x2160 frame over 8 ranks -- emulated on
     one GPU: each rank's buffer, assembled, equals the oracle's frame.  layout "tiles":
-    the 2-D deal bench.py uses (8x16 blocks, block j of band b -> rank (j + 3b) % 8;
+    the 2-D deal bench.py uses (16x16 blocks, block j of band b -> rank (j + 3b) % 8;
     vr_render_tiles + the device assembly kernel), both algorithms; "bands": 8-row bands
     dealt round-robin (vr_render_bands)."""
     import torch
 
     from voxelraymarcher_amd.tiles import assemble_bands
     cfg, xyz, rgb, g, o, frames = c5
-    W, H, R, B, T = cfg.width, cfg.height, 8, 8, 16
+    W, H, R, T = cfg.width, cfg.height, 8, 16
+    B = 16 if layout == "tiles" else 8
     cam, lit = vr.Camera.reference(W, H), vr.setup_constant_values()
     info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
     for algo in (ALGOS if layout == "tiles" else [vr.RayMarchAlgorithm.ORIGINAL]):

@@ -22,7 +22,7 @@ def c1():
 
 
 @pytest.mark.parametrize("R,B,T,stride", [(1, 8, 16, 0), (2, 8, 16, 0), (3, 8, 8, 0), (5, 8, 24, 0), (8, 8, 16, 0),
-                                          (4, 4, 8, 3), (8, 8, 8, 5), (6, 16, 16, 0)])
+                                          (4, 4, 8, 3), (8, 8, 8, 5), (6, 16, 16, 0), (8, 16, 16, 0)])
 @pytest.mark.parametrize("store", [vr.StorageType.VOXEL_CLUSTER_STORE, vr.StorageType.HASH_TABLE],
                          ids=lambda s: s.name)
 def test_tiles_reassemble(c1, R, B, T, stride, store):

@@ -15,7 +15,7 @@ from voxelraymarcher_amd.tiles import (assemble_tiles, deal_stride, tile_local_w
                                        tile_source_index, tile_words)
 
 CASES = [(64, 45, 8, 16, 2), (64, 45, 8, 16, 3), (200, 150, 8, 8, 5), (97, 41, 4, 24, 8), (3840, 2160, 8, 16, 8),
-         (1920, 1080, 8, 16, 4), (33, 7, 3, 5, 6), (16, 8, 8, 16, 1)]
+         (1920, 1080, 8, 16, 4), (33, 7, 3, 5, 6), (16, 8, 8, 16, 1), (3840, 2160, 16, 16, 8)]
 
 
 @pytest.mark.parametrize("W,H,B,T,R", CASES)
