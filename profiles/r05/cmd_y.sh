@@ -1,0 +1,15 @@
+#!/bin/bash
+# Lane-order weight max(p, s) + (p + s) / 8 from separate primary / shadow walk lengths
+# (variant build): parity against it, then A/B against the current library on C2-C5.
+set -o pipefail
+O=${1:-gpurun_out/r05y}
+mkdir -p $O
+export TMPDIR=/tmp
+L=voxelraymarcher_amd/libvr.so
+P=${P:-voxelraymarcher_amd/ab/libvr_pkey2.so}
+VR_LIBRARY=$PWD/$P timeout -k 10 900 python -u -m pytest tests/test_gpu_order.py tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_tiles_deal.py -m gpu -q -x --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for C in ${CFGS:-C2 C3 C4 C5}; do
+  timeout -k 10 600 python profiles/r05/ab_bench.py $C $L $P --rounds 2 > $O/ab_$C.txt 2>&1 || { tail -5 $O/ab_$C.txt; exit 1; }
+  cat $O/ab_$C.txt
+done

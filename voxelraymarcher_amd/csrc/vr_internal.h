@@ -132,7 +132,8 @@ struct KView {
     // Lane order (round 5, vr_march.hip lane_pixel): per pixel block (16x16 by default) the slot
     // of each pixel, dealing them to the block's waves heaviest first (or null: 8x8 tiles;
     // vr::perm_bytes(gx, gy) bytes); pcost (or null): each lane
-    // writes its pixel's walk length (loop iterations) at [l * LW + x], for the next lane order.
+    // writes its pixel's walk lengths at [l * LW + x] (primary << 16 | shadow, each saturated at
+    // 0xFFFF; loop iterations), for the next lane order.
     const uint8_t* perm;
     uint32_t* pcost;
 };

@@ -324,6 +324,13 @@ __device__ __forceinline__ uint32_t* tile_pixels() {
     return p;
 }
 
+// The primary walk's length per tile-pass thread, for a launch that records the lane order's
+// walk lengths (KView::pcost): shade writes it between the walks, march_kernel reads it back.
+__device__ __forceinline__ uint32_t* tile_prim() {
+    __shared__ uint32_t p[64u * kTilesX * kTilesY];
+    return p;
+}
+
 // CRAWL: fast-forward cluster-skip crawls (the deferred-ray pass); otherwise a
 // crawling ray reserves an entry in the launch's deferral list and unwinds.
 // kExact (the crawl pass): every walk runs to its end here, and a loop round that
@@ -1572,7 +1579,9 @@ __device__ __forceinline__ uint32_t shade(const KScene& s, const KView& v, uint3
         Walker<STORE, COUNT, CRAWL> w(s, v);
         attach(w, cl);
         Hit h;
-        if (w.template primary<ALGO>(ro, rd, h)) col = light_and_shadow(w, v, h);
+        const bool hit = w.template primary<ALGO>(ro, rd, h);
+        if (!CRAWL && v.pcost) tile_prim()[threadIdx.x] = w.iters;   // (the lane order's primary walk length)
+        if (hit) col = light_and_shadow(w, v, h);
         if (iters) *iters = w.iters;              // the walk's length (the work order's cost)
         bytes = w.bytes + 4u;                     // + the pixel write
         if (ff) *ff = uint2{w.ff, w.nl};
@@ -1679,6 +1688,7 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, (TileWaves<ALGO, HI>::value
     uint32_t x, l;
     lane_pixel(v, x, l);
     tile_pixels()[threadIdx.x] = (l << 16) | x;     // (read back only by this lane: no barrier)
+    if (v.pcost) tile_prim()[threadIdx.x] = 0u;
     uint32_t bytes = 0, iters = 0;
     if (x < v.LW && l < v.local_rows) {
         // (&iters unconditionally: a pointer chosen by `v.cost ? &iters : nullptr` keeps
@@ -1690,7 +1700,10 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, (TileWaves<ALGO, HI>::value
         const uint32_t p = tile_pixels()[threadIdx.x];
         const size_t at = (size_t)(p >> 16) * v.LW + (p & 0xFFFFu);
         v.out[at] = c;
-        if (v.pcost) v.pcost[at] = iters;         // the pixel's walk length, for the next lane order
+        if (v.pcost) {                            // the pixel's walk lengths, for the next lane order
+            const uint32_t p0 = tile_prim()[threadIdx.x];
+            v.pcost[at] = min(p0, 0xFFFFu) << 16 | min(iters - p0, 0xFFFFu);
+        }
     }
     if (COUNT) add_bytes(v, lane, bytes);
     if (v.cost) {                                  // the wave's walk length, for the next work order
@@ -1710,9 +1723,9 @@ __global__ __launch_bounds__(64 * kTilesX * kTilesY, (TileWaves<ALGO, HI>::value
 // rank in its wave plus, for each other wave, the number of that wave's sorted keys above it
 // (independent binary searches in LDS).  The block's slots are gathered in LDS and stored as
 // words.  With cost non-null the kernel also writes each wave's walk length under the new
-// lane order (KView::cost's layout: the key at rank 64 q is slot q's maximum; blocks cut by
-// the grid's edge keep the 8x8 tiles and write each tile's maximum), so the work order made
-// from them next matches the lane order.
+// lane order -- KView::cost's layout; max(primary) + max(shadow) over the wave's pixels, what
+// the wave runs; blocks cut by the grid's edge keep the 8x8 tiles and write each tile's -- so
+// the work order made from them next matches the lane order.
 constexpr uint32_t kLaneShift = kLaneBlock == 16 ? 8u : 10u;
 __global__ __launch_bounds__(kLanePixels) void perm_kernel(const uint32_t* __restrict__ pcost, uint32_t LW,
                                                            uint32_t rows, uint32_t gx, uint32_t gy,
@@ -1720,21 +1733,40 @@ __global__ __launch_bounds__(kLanePixels) void perm_kernel(const uint32_t* __res
     constexpr uint32_t kWaves = kLanePixels / 64u, kTiles = (kLaneBlock / 8u) * (kLaneBlock / 8u);
     __shared__ uint32_t sorted[kLanePixels];
     __shared__ __attribute__((aligned(16))) PermT slots[kLanePixels];
+    __shared__ uint32_t wmax[2u * kWaves];   // per wave slot (or 8x8 tile): max primary, max shadow
+    __shared__ uint32_t ps[kLanePixels];     // the pixels' walk lengths (cost writes only)
+    static_assert(kTiles == kWaves, "one 8x8 tile per wave slot");
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     const uint32_t nbx = (gx + kLbX - 1u) / kLbX, BX = blockIdx.x % nbx, BY = blockIdx.x / nbx;
     const uint32_t px = t % kLaneBlock, py = t / kLaneBlock;
     const uint32_t x = BX * kLaneBlock + px, l = BY * kLaneBlock + py;
-    const uint32_t c = (x < LW && l < rows) ? min(pcost[(size_t)l * LW + x], (1u << (32u - kLaneShift)) - 1u) : 0u;
+    // a pixel's weight: a wave runs its primary walks until the slowest ends, then its shadow
+    // walks, so it costs max(primary) + max(shadow) over its lanes; max(p, s) + (p + s) / 8
+    // groups lanes best of the weights tried on the oracle's C2 counts (1.4 % fewer
+    // wave-iterations than p + s, profiles/r05/lane_sort_sim.py)
+    uint32_t p = 0, s = 0;
+    if (x < LW && l < rows) {
+        const uint32_t w = pcost[(size_t)l * LW + x];
+        p = w >> 16;
+        s = w & 0xFFFFu;
+    }
+    const uint32_t c = min(max(p, s) + ((p + s) >> 3), (1u << (32u - kLaneShift)) - 1u);
+    if (cost) {
+        if (t < 2u * kWaves) wmax[t] = 0u;
+        ps[t] = p << 16 | s;
+    }
     if ((BX + 1u) * kLbX > gx || (BY + 1u) * kLbY > gy) {
-        if (cost) {                 // the block's 8x8 tiles that exist: their maxima
-            if (t < kTiles) sorted[t] = 0u;
+        if (cost) {                 // the block's 8x8 tiles that exist
             __syncthreads();
-            atomicMax(&sorted[(py >> 3) * (kLaneBlock / 8u) + (px >> 3)], c);
+            const uint32_t ti = (py >> 3) * (kLaneBlock / 8u) + (px >> 3);
+            atomicMax(&wmax[ti], p);
+            atomicMax(&wmax[kWaves + ti], s);
             __syncthreads();
             if (t < kTiles) {
                 const uint32_t tx = t % (kLaneBlock / 8u), ty = t / (kLaneBlock / 8u);
                 const uint32_t col = BX * kLbX + tx / kTilesX, row = BY * kLbY + ty;
-                if (col < gx && row < gy) cost[(row * gx + col) * kWavesPerTileGroup + tx % kTilesX] = sorted[t];
+                if (col < gx && row < gy)
+                    cost[(row * gx + col) * kWavesPerTileGroup + tx % kTilesX] = wmax[t] + wmax[kWaves + t];
             }
         }
         return;
@@ -1752,20 +1784,26 @@ __global__ __launch_bounds__(kLanePixels) void perm_kernel(const uint32_t* __res
     uint32_t rank = lane;
 #pragma unroll
     for (uint32_t o = 1; o < kWaves; ++o) {
-        const uint32_t* s = sorted + (((wave + o) % kWaves) << 6);
-        uint32_t lo = 0;            // the number of s's keys above key (s descending)
+        const uint32_t* sw = sorted + (((wave + o) % kWaves) << 6);
+        uint32_t lo = 0;            // the number of sw's keys above key (sw descending)
 #pragma unroll
         for (uint32_t step = 32; step > 0; step >>= 1)
-            if (s[lo + step - 1u] > key) lo += step;
-        rank += lo + (s[63] > key ? 1u : 0u);     // (all 64 above: lo stops at 63)
+            if (sw[lo + step - 1u] > key) lo += step;
+        rank += lo + (sw[63] > key ? 1u : 0u);    // (all 64 above: lo stops at 63)
     }
-    slots[rank] = (PermT)(key & (kLanePixels - 1u));
-    if (cost && (rank & 63u) == 0u) {
-        const uint32_t q = rank >> 6, g = q / kTilesX;
-        const uint32_t col = BX * kLbX + g % kLbX, row = BY * kLbY + g / kLbX;
-        cost[(row * gx + col) * kWavesPerTileGroup + q % kTilesX] = key >> kLaneShift;
+    const uint32_t pix = key & (kLanePixels - 1u);
+    slots[rank] = (PermT)pix;
+    if (cost) {                     // the walk lengths of the pixel this thread's key carries
+        const uint32_t w = ps[pix];
+        atomicMax(&wmax[rank >> 6], w >> 16);
+        atomicMax(&wmax[kWaves + (rank >> 6)], w & 0xFFFFu);
     }
     __syncthreads();
+    if (cost && t < kWaves) {
+        const uint32_t g = t / kTilesX;
+        const uint32_t col = BX * kLbX + g % kLbX, row = BY * kLbY + g / kLbX;
+        cost[(row * gx + col) * kWavesPerTileGroup + t % kTilesX] = wmax[t] + wmax[kWaves + t];
+    }
     constexpr uint32_t kWords = kLanePixels * sizeof(PermT) / 4u;
     uint32_t* out = reinterpret_cast<uint32_t*>(perm + (size_t)blockIdx.x * kLanePixels * sizeof(PermT));
     if (t < kWords) out[t] = reinterpret_cast<const uint32_t*>(slots)[t];
