@@ -9,7 +9,7 @@ roofline of the dominant kernel and the CPU oracle baseline.
 A step = one full frame.  With N > 1 ranks the frame is dealt over the ranks --
 fixed tiling: the 2-D tile deal (every 16-row band cut into 16-column blocks, block j
 of band b -> rank (j + 3b) % N, so expensive rows are spread over every rank; --layout
-bands keeps whole 8-row bands, band b -> rank b % N); weak tiling: 8-row bands -- each
+bands keeps whole 16-row bands, band b -> rank b % N); weak tiling: 16-row bands -- each
 rank renders its share and every frame is gathered to rank 0 over RCCL as RGB8 (3 B
 per pixel) and assembled there.  Tiling:
   fixed -- the config's own frame whatever N is (strong scaling; BASELINE C5 is
@@ -91,7 +91,7 @@ def parse():
     p.add_argument("--resolution", default="",
                    help="WxH instead of the config's frame (tests; the same view and scene)")
     p.add_argument("--layout", default="auto", choices=["auto", "bands", "tiles"],
-                   help="how the frame is dealt over N > 1 ranks: 8-row bands, or the 2-D tile deal (16-row bands "
+                   help="how the frame is dealt over N > 1 ranks: 16-row bands, or the 2-D tile deal (16-row bands "
                         "cut into --tile-cols column blocks); auto = tiles for fixed tiling, bands for weak")
     p.add_argument("--tile-cols", type=int, default=16, help="column block of the 2-D tile deal (one workgroup)")
     p.add_argument("--exchange", action="store_true",
@@ -131,9 +131,9 @@ from voxelraymarcher_amd.tiles import BandGather, frame_resolution, init_frame_g
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 N_SIMD = 1024              # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles (SIMD-32)
-BAND_ROWS = 8              # row bands: one wave tile high
-TILE_BAND_ROWS = 16        # 2-D tile deal: a 16x16 block per deal unit, one lane-order block
-                           # (8-row bands put two frame strips in one block: C5 rank 0.099 vs 0.089 ms)
+BAND_ROWS = 16             # row bands and the 2-D tile deal's bands: one 16x16 lane-order block high
+                           # (8-row bands put two frame strips in one block: C5 rank of 8 0.099 vs
+                           # 0.089 ms, C2 weak rank of 8 0.0883 vs 0.0841)
 HEADLINE = "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s"   # BASELINE.json metric
 
 
@@ -275,7 +275,7 @@ def main():
     # pixel): rank 0 ends each frame with the RGB8 image
     depth = args.frames_in_flight or pipeline_depth(args.config)
     layout = args.layout if args.layout != "auto" else ("tiles" if tiling == "fixed" else "bands")
-    band_rows = TILE_BAND_ROWS if layout == "tiles" else BAND_ROWS
+    band_rows = BAND_ROWS
     pipe = BandGather(W, H, band_rows, rank, world, dev, depth=depth, rgb8=grouped, stage_host=stage_host,
                       tile_cols=args.tile_cols if layout == "tiles" else 0, exchange=grouped)
     tcols = pipe.T          # 0: row bands (every N = 1 run without --exchange)

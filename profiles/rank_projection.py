@@ -29,11 +29,13 @@ p.add_argument("--steps", type=int, default=100)
 p.add_argument("--warmup", type=int, default=20)
 p.add_argument("--frames-in-flight", type=int, default=0, help="default: tiles.pipeline_depth (bench.py's)")
 p.add_argument("--ranks", default="", help="comma-separated subset of ranks (default: all)")
-p.add_argument("--band-rows", type=int, default=0, help="default: 16 for the tile deal (bench.py), 8 for bands")
+p.add_argument("--band-rows", type=int, default=16, help="bench.py's BAND_ROWS")
 p.add_argument("--layout", default="tiles", choices=["tiles", "bands"],
                help="tiles: the 2-D deal bench.py uses for fixed tiling (round 5); bands: 8-row bands")
 p.add_argument("--tile-cols", type=int, default=16)
 p.add_argument("--latency-reps", type=int, default=30)
+p.add_argument("--tiling", default="fixed", choices=["fixed", "weak"],
+               help="weak: the frame bench.py --tiling weak renders at --world ranks (each side x sqrt(N))")
 a = p.parse_args()
 
 from voxelraymarcher_amd.tiles import pipeline_depth, pipeline_hw_queues  # noqa: E402  (no GPU yet)
@@ -53,10 +55,13 @@ dev = torch.device("cuda", 0)
 xyz, rgb = cfg.voxels()
 scene = vr.create_scene(xyz, rgb, cfg.store)
 W, H = cfg.width, cfg.height
+if a.tiling == "weak":
+    from voxelraymarcher_amd.tiles import frame_resolution
+    W, H = frame_resolution(W, H, a.world, "weak")
 cam = vr.Camera.reference(W, H)
 lit = vr.setup_constant_values()
 info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
-B = a.band_rows or (16 if a.layout == "tiles" else 8)
+B = a.band_rows
 T = a.tile_cols if a.layout == "tiles" else 0
 words = vr.tile_buffer_words(W, H, B, T, a.world) if T else vr.band_buffer_words(W, H, B, a.world)
 
