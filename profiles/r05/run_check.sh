@@ -23,7 +23,15 @@ for C in "${CFGS[@]}"; do
   mkdir -p $O/prof_$C
   timeout -s KILL 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof_$C -o run -- python3 bench.py --config $C --no-cpu-baseline > $O/bench_$C.json 2> $O/bench_$C.err || { tail -5 $O/bench_$C.err; exit 1; }
   python3 profiles/roofline_phases.py $O/prof_$C/run_kernel_trace.csv $O/bench_$C.json $O/prof_$C > $O/phases_$C.txt || exit 1
-  echo "$C: $(python3 -c "import json,sys; d=json.loads(open('$O/bench_$C.json').read().strip().splitlines()[-1]); r=d['roofline']; print(d['value'], d['ms_per_step'], d['kernel_ms'], d['kernel_ms_grid_order'], r['frac'], r['frac_learned_order'], r['frac_pipelined'], r['crawl_iterations_fast_forwarded'])")"
+  echo "$C: $(python3 -c "import json,sys; d=json.loads(open('$O/bench_$C.json').read().strip().splitlines()[-1]); r=d['roofline']; print(d['value'], d['ms_per_step'], d['kernel_ms'], d['kernel_ms_grid_order'], d.get('kernel_ms_first_render'), r['frac'], r.get('frac_grid_order'), r['frac_learned_order'], r['frac_pipelined'], r['crawl_iterations_fast_forwarded'])")"
   cat $O/phases_$C.txt
   rm -f $O/prof_$C/run_kernel_trace.csv.gz; gzip -f $O/prof_$C/run_kernel_trace.csv
 done
+# the CPU baseline per config (the driver line carries C2's): bench.py without rocprofv3
+if [ $TESTS = 1 ]; then
+  for C in "${CFGS[@]}"; do
+    [ $C = C2 ] && continue
+    timeout -k 10 400 python bench.py --config $C > $O/bench_cpu_$C.json 2> $O/bench_cpu_$C.err || { tail -5 $O/bench_cpu_$C.err; exit 1; }
+    echo "$C cpu: $(python3 -c "import json; d=json.loads(open('$O/bench_cpu_$C.json').read().strip().splitlines()[-1]); print(d['value'], d['cpu_baseline'])")"
+  done
+fi
