@@ -3,12 +3,17 @@
 # per config a rocprofv3 kernel trace of ONE bench.py run whose JSON line it splits into
 # the run's dispatch phases (profiles/roofline_phases.py: every roofline fraction of the
 # line recomputed from the trace).
-#   bash profiles/r05/run_check.sh <out> [configs...] [--no-tests]
+#   bash profiles/r05/run_check.sh <out> [configs...] [--no-tests] [--cpu]
+# (--cpu: also each config's bench line with its CPU baseline, without rocprofv3; C2's is the
+# driver line's)
 set -o pipefail
 O=$1; shift
 TESTS=1
+CPU=0
 CFGS=()
-for a in "$@"; do if [ "$a" = "--no-tests" ]; then TESTS=0; else CFGS+=("$a"); fi; done
+for a in "$@"; do
+  if [ "$a" = "--no-tests" ]; then TESTS=0; elif [ "$a" = "--cpu" ]; then CPU=1; else CFGS+=("$a"); fi
+done
 [ ${#CFGS[@]} -eq 0 ] && CFGS=(C2 C3 C4 C5)
 mkdir -p $O
 export TMPDIR=/tmp
@@ -28,7 +33,7 @@ for C in "${CFGS[@]}"; do
   rm -f $O/prof_$C/run_kernel_trace.csv.gz; gzip -f $O/prof_$C/run_kernel_trace.csv
 done
 # the CPU baseline per config (the driver line carries C2's): bench.py without rocprofv3
-if [ $TESTS = 1 ]; then
+if [ $CPU = 1 ]; then
   for C in "${CFGS[@]}"; do
     [ $C = C2 ] && continue
     timeout -k 10 400 python bench.py --config $C > $O/bench_cpu_$C.json 2> $O/bench_cpu_$C.err || { tail -5 $O/bench_cpu_$C.err; exit 1; }
