@@ -564,11 +564,10 @@ struct SlotRing {
             uint32_t cap = 0, gx = 0, gy = 0, age = 0;
             uint64_t key = 0;              // the view it was learned on (view_key)
             bool valid = false;
-            // the lane order (vr_march.hip lane_pixel): per-pixel walk lengths and, per 16x16
-            // block, its pixels heaviest first, for a grid of lgx x lgy
-            uint32_t* pcost = nullptr;     // one word per pixel of the view
+            // the lane order (vr_march.hip lane_pixel): per 16x16 block its pixels heaviest
+            // first, for a grid of lgx x lgy, learned on view lkey
             uint8_t* perm = nullptr;       // vr::perm_bytes(lgx, lgy)
-            size_t pcap = 0, bcap = 0;
+            size_t bcap = 0;
             uint32_t lgx = 0, lgy = 0, lage = 0;
             uint64_t lkey = 0;
             bool lvalid = false;
@@ -819,35 +818,31 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // view repeats.  It permutes pixels within 16x16 blocks only: any permutation renders the
     // same pixels.
     bool relane = false;
+    uint32_t* pcost = nullptr;        // (a relaning launch's per-pixel walk lengths: transient)
     const size_t npx = (size_t)v.LW * v.local_rows, nperm = vr::perm_bytes(gx, gy);
     if (lane_order_enabled() && n != 0) {
-        if (npx > O.pcap || nperm > O.bcap) {
-            hipError_t e = hipSuccess;
-            if (O.pcost) e = hipFreeAsync(O.pcost, st);
-            if (O.perm) {
-                const hipError_t e2 = hipFreeAsync(O.perm, st);
-                if (e == hipSuccess) e = e2;
-            }
-            O.pcost = nullptr;
+        if (nperm > O.bcap) {
+            hipError_t e = O.perm ? hipFreeAsync(O.perm, st) : hipSuccess;
             O.perm = nullptr;
-            O.pcap = O.bcap = 0;
+            O.bcap = 0;
             O.lvalid = false;
-            if (e == hipSuccess) e = hipMallocAsync((void**)&O.pcost, sizeof(uint32_t) * npx, st);
             if (e == hipSuccess) e = hipMallocAsync((void**)&O.perm, nperm, st);
             if (e != hipSuccess) {
-                if (O.pcost) (void)hipFreeAsync(O.pcost, st);
-                if (O.perm) (void)hipFreeAsync(O.perm, st);
-                O.pcost = nullptr;
                 O.perm = nullptr;
-                return hip_fail(e, "lane order buffers");
+                return hip_fail(e, "lane order buffer");
             }
-            O.pcap = npx;
             O.bcap = nperm;
         }
         const bool match = O.lvalid && O.lgx == gx && O.lgy == gy && O.lkey == key;
         v.perm = match ? O.perm : nullptr;
         relane = match ? refresh_due(O.lage) : repeat;
-        v.pcost = relane ? O.pcost : nullptr;
+        if (relane) {
+            // 4 B per pixel, only between this launch's tile pass and its perm_kernel (freed
+            // stream-ordered after it): the slots keep 1 B per pixel each, not 5
+            const hipError_t e = hipMallocAsync((void**)&pcost, sizeof(uint32_t) * npx, st);
+            if (e != hipSuccess) return hip_fail(e, "lane order walk lengths");
+        }
+        v.pcost = pcost;
     }
     // crawl pass grid from the records an earlier launch deferred (a hint: any grid renders
     // the same pixels)
@@ -866,7 +861,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     bool with_costs = false;
     if (e == hipSuccess && relane) {
         with_costs = order_enabled() && O.cost && O.cap >= n;
-        e = vr::launch_perm(O.pcost, v.LW, v.local_rows, gx, gy, O.perm, with_costs ? O.cost : nullptr, st);
+        e = vr::launch_perm(pcost, v.LW, v.local_rows, gx, gy, O.perm, with_costs ? O.cost : nullptr, st);
         O.lvalid = e == hipSuccess;
         O.relaned = !with_costs;
         O.lgx = gx;
@@ -899,6 +894,10 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         O.key = key;
         O.age = 0;
         O.relaned = false;
+    }
+    if (pcost) {
+        const hipError_t ef = hipFreeAsync(pcost, st);
+        if (e == hipSuccess) e = ef;
     }
     // (on a failed launch the slot is still fenced: a kernel of it may be queued)
     rc = lease.release(st);
