@@ -698,6 +698,14 @@ bool lane_order_enabled() {
     }();
     return on;
 }
+// VR_INFLIGHT_HEAVY=1 (A/B runs): AUTO dispatches heaviest first with frames in flight too.
+bool inflight_heavy() {
+    static const bool on = [] {
+        const char* e = std::getenv("VR_INFLIGHT_HEAVY");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 bool order_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("VR_ORDER");
@@ -763,7 +771,8 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     bool remake = false;
     // (the lock orders launches: "previous" is well defined)
     const bool alone = !D.any || D.last_stream == st || hipEventQuery(D.ev[D.last_idx]) == hipSuccess;
-    const bool heavy = schedule == VR_SCHEDULE_HEAVIEST_FIRST || (schedule == VR_SCHEDULE_AUTO && alone);
+    const bool heavy = schedule == VR_SCHEDULE_HEAVIEST_FIRST ||
+                       (schedule == VR_SCHEDULE_AUTO && (alone || inflight_heavy()));
     // crawl records per wave: a lone frame ends with the crawl pass's longest chain (2 per
     // wave since round 4's shorter chains: C5 alone 0.767 -> 0.759 ms vs 4,
     // profiles/r04/crawl/scene_lds_ab.txt, rpw_multi_cluster.txt); with frames in flight the
