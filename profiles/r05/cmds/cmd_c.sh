@@ -9,4 +9,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout
 tail -2 $O/tests.log
 timeout -k 10 600 python profiles/r05/ab_bench.py C4 voxelraymarcher_amd/libvr.so voxelraymarcher_amd/ab/libvr_nofilter.so --rounds 2 > $O/ab_filter_C4.txt 2>&1 || { tail -5 $O/ab_filter_C4.txt; exit 1; }
 cat $O/ab_filter_C4.txt
-bash profiles/r05/cmd_b.sh $O/b
+bash profiles/r05/cmds/cmd_b.sh $O/b

@@ -13,4 +13,4 @@ timeout -k 10 600 python profiles/r05/ab_bench.py C5 $L:VR_SPARSE=0 $L:VR_SPARSE
 cat $O/ab_sparse_C5.txt
 timeout -k 10 600 python profiles/r05/ab_bench.py C2 $L $L:VR_SPARSE=1 $L:VR_PRIO_HEAD_DIV=32 $L:VR_PRIO_HEAD_DIV=8 $L:VR_PRIO_ESC=64 $L:VR_PRIO_ESC=128 --rounds 2 > $O/ab_prio_C2.txt 2>&1 || { tail -5 $O/ab_prio_C2.txt; exit 1; }
 cat $O/ab_prio_C2.txt
-bash profiles/r05/cmd_d.sh $O/d
+bash profiles/r05/cmds/cmd_d.sh $O/d
