@@ -79,3 +79,34 @@ def test_tiles_counted_bytes_sum_to_the_frame(c1):
     # every pixel of the buffers past the frame counts nothing; every frame pixel once
     assert total == full
     scene.close()
+
+
+@pytest.mark.parametrize("R", [3, 8])
+def test_tiles_with_learned_orders(c1, R):
+    """Each rank's tile buffer rendered 40 times in a row (so the slots learn its work and lane
+    orders, include/vr.h vr_forget_orders) equals its first render, for the 16x16 deal bench.py
+    uses and both algorithms; the assembled frame of the last renders equals the full render."""
+    cfg = vr.CONFIGS["C1"]
+    W, H, B, T = 203, 150, 16, 16
+    scene = vr.create_scene(*c1, vr.StorageType.VOXEL_CLUSTER_STORE)
+    cam, lit, info = vr.Camera.reference(W, H), vr.setup_constant_values(), vr.VoxelSceneInfo((0, 0, 0), cfg.scale)
+    for algo in (vr.RayMarchAlgorithm.ORIGINAL, vr.RayMarchAlgorithm.LONGEST_AXIS):
+        full, _ = gpu_render(scene, algo, cam, lit, info, W, H)
+        words = vr.tile_buffer_words(W, H, B, T, R)
+        parts = torch.full((R, words), -7, dtype=torch.int32, device="cuda")
+        for r in range(R):
+            first = None
+            for i in range(40):
+                buf = torch.full((words,), -7, dtype=torch.int32, device="cuda")
+                vr.render_tiles(scene, algo, cam, lit, info, W, H, B, T, r, R, buf)
+                torch.cuda.synchronize()
+                if first is None:
+                    first = buf.clone()
+                assert torch.equal(buf, first), (algo.name, R, r, i)
+            parts[r] = first
+        frame = torch.full((H, W), -9, dtype=torch.int32, device="cuda")
+        vr.assemble_tiles_device(parts, frame, 4, W, H, B, T, R)
+        torch.cuda.synchronize()
+        img = frame.cpu().numpy().view(np.uint32).reshape(-1)
+        assert np.array_equal(img, full), f"{algo.name} R={R}: " + diff_report(img, full, W)
+    scene.close()
