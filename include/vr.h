@@ -267,8 +267,10 @@ typedef enum {
  * Both are learned from the walk lengths of earlier launches of the SAME view (scene,
  * algorithm, camera, lights, transform, frame size, rows and band / tile deal) on the device
  * and used only for that view: a view's first launches, and a view that changes on every
- * launch, render with neither.  Neither ever changes a pixel.  vr_forget_orders drops
- * what a device has learned, so the next launch renders as a first render (measurement). */
+ * launch, render with neither.  Neither ever changes a pixel.  A slot that has seen a view
+ * defer no walk to the crawl pass skips that view's crawl pass (records carry their launch,
+ * so a wrong skip could never shade another frame's pixels).  vr_forget_orders drops what a
+ * device has learned, so the next launch renders as a first render (measurement). */
 int vr_forget_orders(int device);
 /* Every vr_render* call returns VR_E_INVALID on a stream that is capturing a HIP graph
  * (its per-device slot ring and work-order bookkeeping are host state that a graph replay

@@ -554,8 +554,11 @@ struct SlotRing {
         std::vector<hipEvent_t> ev;
         std::vector<bool> used;
         uint32_t next = 0;
-        uint32_t* stat_host = nullptr;     // host-mapped: the last crawl pass's record count
+        // host-mapped: [0] the last crawl pass's record count (any slot); then per slot the
+        // {launch id, record count} its last crawl pass reported (two words, 8-B aligned)
+        uint32_t* stat_host = nullptr;
         uint32_t* stat_dev = nullptr;
+        uint32_t launch_serial = 0;
         // per slot: the tile pass's work order (heaviest tile groups first) made from the
         // costs of the slot's last launch that recorded them, for a grid of gx x gy
         struct Order {
@@ -572,6 +575,11 @@ struct SlotRing {
             uint64_t lkey = 0;
             bool lvalid = false;
             bool relaned = false;          // the lane order changed after the work order's costs
+            // the crawl pass: the slot's last launch that ran one (id, view), and whether a
+            // completed one reported that this view defers nothing
+            uint32_t cid = 0;
+            uint64_t ckey = 0;
+            bool czero = false;
         };
         std::vector<Order> ord;
         bool any = false;                  // the device's previous launch: its stream and slot
@@ -607,9 +615,10 @@ int ring_init(SlotRing& r, SlotRing::Dev& D) {
     }
     void* h = nullptr;
     void* hd = nullptr;
-    e = hipHostMalloc(&h, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent);
+    const size_t stat_words = 2u + 2u * (size_t)r.nslots;
+    e = hipHostMalloc(&h, sizeof(uint32_t) * stat_words, hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) {
-        *(volatile uint32_t*)h = 0u;
+        for (size_t i = 0; i < stat_words; ++i) ((volatile uint32_t*)h)[i] = 0u;
         e = hipHostGetDevicePointer(&hd, h, 0);
         if (e != hipSuccess) (void)hipHostFree(h);
     }
@@ -703,6 +712,14 @@ bool inflight_heavy() {
     static const bool on = [] {
         const char* e = std::getenv("VR_INFLIGHT_HEAVY");
         return e && e[0] == '1';
+    }();
+    return on;
+}
+// VR_CRAWL_SKIP=0 (A/B runs): every launch runs its crawl pass.
+bool crawl_skip_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("VR_CRAWL_SKIP");
+        return !(e && e[0] == '0');
     }();
     return on;
 }
@@ -853,6 +870,30 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
         }
         v.pcost = pcost;
     }
+    // The crawl pass is skipped for a view this slot has seen defer nothing: whether a walk
+    // is deferred is a pure function of its ray, so a view defers the same pixels on every
+    // launch.  Every record carries its launch's id and a crawl pass shades only its own,
+    // so even a wrong skip cannot put another frame's pixels into a frame; the records it
+    // leaves raise the count the next crawl pass of the slot reports, which ends the skipping.
+    // (C2 lone launch: the 4-us empty crawl pass and a kernel boundary.)
+    bool crawl = true;
+    {
+        uint32_t lid = ++D.launch_serial;
+        if (lid == 0u) lid = ++D.launch_serial;
+        v.launch_id = lid;
+        if (O.ckey != key) {
+            O.czero = false;
+        } else if (!O.czero && O.cid != 0u) {
+            const uint64_t r = *reinterpret_cast<volatile uint64_t*>(D.stat_host + 2 + 2 * (size_t)lease.idx);
+            O.czero = (uint32_t)r == O.cid && (uint32_t)(r >> 32) == 0u;
+        }
+        crawl = !(O.czero && crawl_skip_enabled());
+        if (crawl) {
+            v.slot_stat = D.stat_dev + 2 + 2 * (size_t)lease.idx;
+            O.cid = lid;
+            O.ckey = key;
+        }
+    }
     // crawl pass grid from the records an earlier launch deferred (a hint: any grid renders
     // the same pixels)
     const vr::KScene ks = kscene(s);
@@ -861,7 +902,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // stream's launch is running
     const bool hi = occupancy == VR_OCCUPANCY_IN_FLIGHT ||
                     (occupancy == VR_OCCUPANCY_AUTO && !alone && in_flight_occupancy());
-    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs, hi);
+    hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs, hi, crawl);
     // The lane order first: when the slot has work-order buffers for this grid, perm_kernel
     // also writes the waves' costs under the new lane order and the work order is remade from
     // them at once -- an order made from costs walked under another lane order puts the light
@@ -1297,7 +1338,10 @@ int vr_forget_orders(int device) {
     if (device < 0 || device >= 64) return fail(VR_E_INVALID, "device index out of range");
     SlotRing::Dev& D = g_defer_ring.dev[device];
     std::lock_guard<std::mutex> lk(D.mu);
-    for (SlotRing::Dev::Order& O : D.ord) O.valid = O.lvalid = O.relaned = false;   // (buffers kept)
+    for (SlotRing::Dev::Order& O : D.ord) {         // (buffers kept)
+        O.valid = O.lvalid = O.relaned = O.czero = false;
+        O.cid = 0;
+    }
     D.last_key = 0;
     return VR_OK;
 }

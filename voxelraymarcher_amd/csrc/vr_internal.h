@@ -136,6 +136,10 @@ struct KView {
     // 0xFFFF; loop iterations), for the next lane order.
     const uint8_t* perm;
     uint32_t* pcost;
+    // (or null) the launch slot's host-mapped crawl report: the crawl pass writes
+    // {launch_id, records deferred} there in one 8-B store (the host's crawl-pass skip)
+    uint32_t* slot_stat;
+    uint32_t launch_id;
 };
 
 // Rays that start a cluster-skip crawl (see vr_march.hip crawl_steps) in the
@@ -161,7 +165,7 @@ constexpr uint32_t kDeferWords = 4 + kDeferCap * kDeferRecWords;
 // in_flight: another stream's launch is still running on the device (the tile pass then
 // takes its higher-occupancy variant where one exists, vr_march.hip TileWaves)
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v,
-                        hipStream_t stream, uint32_t crawl_wgs, bool in_flight);
+                        hipStream_t stream, uint32_t crawl_wgs, bool in_flight, bool crawl = true);
 // Crawl-pass grid for a launch that expects about `records` deferred pixels.
 uint32_t crawl_grid(uint32_t records, uint32_t rpw);
 // vcs_cbits of a VCS scene from its mask records (one thread per 32 cluster slots).

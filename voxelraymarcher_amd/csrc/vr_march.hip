@@ -703,7 +703,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                             r[1] = (SHADOW ? 1u : 0u) | this->ctx;
                             r[2] = __float_as_uint(o.x); r[3] = __float_as_uint(o.y); r[4] = __float_as_uint(o.z);
                             r[5] = (uint32_t)cr.x; r[6] = (uint32_t)cr.y; r[7] = (uint32_t)cr.z;
-                            r[8] = 0u;                                  // (the crawl pass reads it again)
+                            r[8] = v.launch_id;                         // (the crawl pass takes only its launch's)
                             r[9] = this->iters;
                             r[10] = this->bytes;
                             // (a shadow walk has no normal: its t values are not kept live for this)
@@ -1544,6 +1544,7 @@ __device__ __forceinline__ uint32_t defer_rewalk(const KView& v) {
         uint32_t* r = v.defer + 4 + (size_t)idx * kDeferRecWords;
         r[0] = tile_pixels()[threadIdx.x];
         r[1] = 4u;
+        r[8] = v.launch_id;
         return 0u;
     }
     atomicAdd(v.defer + 2, 1u);
@@ -1866,7 +1867,10 @@ __global__ __launch_bounds__(64 * kCrawlWaves) void crawl_kernel(KScene s, KView
     __syncthreads();
     const uint32_t total = dyn[0], overflow = dyn[1];
     // what this launch deferred, for the host's grid size of later launches (a hint only)
-    if (blockIdx.x == 0 && threadIdx.x == 0 && v.defer_stat) *v.defer_stat = total + overflow;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (v.defer_stat) *v.defer_stat = total + overflow;
+        if (v.slot_stat) *reinterpret_cast<uint2*>(v.slot_stat) = uint2{v.launch_id, total + overflow};
+    }
     if (total == 0u && overflow == 0u) return;   // nothing deferred (the usual case): no reset needed
     const uint32_t n = min(total, v.defer_cap);
     CrawlLds cl;
@@ -1884,6 +1888,10 @@ __global__ __launch_bounds__(64 * kCrawlWaves) void crawl_kernel(KScene s, KView
         cl.lbm = dyn + 4 + ((threadIdx.x >> 6) * kCrawlMaxRpw + wlane) * 16u;
     for (uint32_t i = wave * rpw + wlane; wlane < rpw && i < n; i += nwaves * rpw) {
         uint32_t* r = v.defer + 4 + (size_t)i * kDeferRecWords;
+        // (a record of another launch -- one whose crawl pass the host skipped, believing its
+        // view defers nothing -- is not this frame's: never shade it into this frame; its count
+        // in this pass's report stops the skipping)
+        if (r[8] != v.launch_id) continue;
         uint32_t b;
         const uint32_t x = r[0] & 0xFFFFu, l = r[0] >> 16;
         // The crawl iteration's voxel q (see crawl_voxel), recovered from the stepped
@@ -2061,7 +2069,7 @@ hipError_t launch_order(const uint32_t* cost, uint32_t n, uint32_t columns, uint
 }
 
 hipError_t launch_march(int store, int algo, bool count, const KScene& s, const KView& v, hipStream_t stream,
-                        uint32_t crawl_wgs, bool in_flight) {
+                        uint32_t crawl_wgs, bool in_flight, bool crawl) {
     uint32_t gx, gy;
     march_grid(v, gx, gy);
     dim3 grid(gx, gy);
@@ -2073,7 +2081,7 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
 #define VR_LAUNCH_HI(ST, AL, CT, HI)                                                              \
     do {                                                                                           \
         hipLaunchKernelGGL((march_kernel<ST, AL, CT, HI>), grid, block, 0, stream, s, v);          \
-        if (v.defer && !kNoCrawlPass)                                                              \
+        if (v.defer && crawl && !kNoCrawlPass)                                                     \
             hipLaunchKernelGGL((crawl_kernel<ST, AL, CT>), cgrid, cblock, 0, stream, s, v);        \
     } while (0)
 #ifdef VR_ISA_ONLY
