@@ -280,11 +280,30 @@ def main():
                       tile_cols=args.tile_cols if layout == "tiles" else 0, exchange=grouped)
     tcols = pipe.T          # 0: row bands (every N = 1 run without --exchange)
 
-    def render(buf):   # on the current stream (BandGather's slot stream in the loops)
+    def render_with(c, buf):   # on the current stream (BandGather's slot stream in the loops)
         if tcols:
-            vr.render_tiles(scene, cfg.algorithm, cam, lit, info, W, H, band_rows, tcols, rank, world, buf)
+            vr.render_tiles(scene, cfg.algorithm, c, lit, info, W, H, band_rows, tcols, rank, world, buf)
         else:
-            vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, band_rows, rank, world, buf)
+            vr.render_bands(scene, cfg.algorithm, c, lit, info, W, H, band_rows, rank, world, buf)
+
+    def render(buf):
+        render_with(cam, buf)
+
+    # A moving view: the same camera with its eye moved by 1, 2 and 3 ulps in x,
+    # one per frame in turn, so no two consecutive launches -- and no launch slot's successive
+    # uses (16 slots, 3 views) -- see the same view: nothing is learned (no work or lane order,
+    # no crawl-pass skip), every frame renders as a first render does, as for a moving camera.
+    moving = []
+    for k in (1, 2, 3):
+        c = vr.Camera.reference(W, H)
+        bits = np.array([c.raw.origin[0]], dtype=np.float32).view(np.uint32) + np.uint32(k)
+        c.raw.origin[0] = float(bits.view(np.float32)[0])
+        moving.append(c)
+    moving_step = [0]
+
+    def render_moving(buf):
+        render_with(moving[moving_step[0] % 3], buf)
+        moving_step[0] += 1
 
     # algorithmic bytes of THIS rank's launch (its bands; instrumented kernel,
     # untimed) and of the whole frame (sum over ranks); `stats`: the part of
@@ -385,6 +404,18 @@ def main():
     if args.dump_frame and rank == 0:
         np.save(args.dump_frame, pipe.last_frame().cpu().numpy())
 
+    # the same pipelined loop with the moving view (nothing learned; after the timed loop)
+    barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.step(render_moving)
+    pipe.drain()
+    torch.cuda.synchronize()
+    barrier()
+    dt_mov = allreduce(time.perf_counter() - t1, op=dist.ReduceOp.MAX)
+    ms_moving = dt_mov / args.steps * 1e3
+
     if rank == 0:
         def gbs(nbytes, ms):
             return nbytes / (ms * 1e-3) / 1e9
@@ -413,6 +444,7 @@ def main():
                 "frac_grid_order": round(gbs(issued_bytes, kern_grid_ms) / HBM_PEAK_GBS, 4),
                 "frac_learned_order": round(gbs(issued_bytes, kern_ms) / HBM_PEAK_GBS, 4),
                 "frac_pipelined": round(gbs(issued_bytes, ms_per_step) / HBM_PEAK_GBS, 4),
+                "frac_pipelined_moving_view": round(gbs(issued_bytes, ms_moving) / HBM_PEAK_GBS, 4),
                 "frac_section8d": round(gbs(launch_bytes, kern_first_ms) / HBM_PEAK_GBS, 4),
                 "fracs_basis": "the same issued bytes over kernel_ms_grid_order (one launch alone in grid order "
                                "with the lane order learned from earlier launches of the view), kernel_ms (one "
@@ -420,7 +452,13 @@ def main():
                                "frame rate); frac_section8d: the full SURVEY 8(d) count over "
                                "kernel_ms_first_render (crawl iterations credited as if loaded). "
                                "profiles/roofline_phases.py recomputes frac, frac_grid_order and "
-                               "frac_learned_order from a rocprofv3 kernel trace of the same run",
+                               "frac_learned_order from a rocprofv3 kernel trace of the same run. "
+                               "frac_pipelined_moving_view: over ms_per_step_moving_view (nothing learned). "
+                               "Every frac here is a REFERENCE-EQUIVALENT WORD RATE, cache-served: the 4-B words "
+                               "the reference walk reads, answered by 8-B mask-record loads that mostly hit the "
+                               "vector L1 / L2 (the scene is L2/MALL-resident), over the HBM peak as SURVEY 8(d) "
+                               "defines the roofline -- not HBM traffic (hbm_measured_frac is); above 1 it is "
+                               "cache-served words, and the roof that binds is bound / bound_frac",
                 }
         hbm_frac = valu_frac = None
         if traffic:
@@ -453,6 +491,23 @@ def main():
             roof["bound"] = "valu" if valu_frac >= hbm_frac else "hbm"
             roof["bound_basis"] = ("the measured limiter: VALU issue fraction vs measured HBM fraction "
                                    f"({valu_frac:.3f} vs {hbm_frac:.3f}, profiles/traffic.json)")
+            # how close the kernel is to the roof that binds: for VALU the share of the chip's
+            # lane-slots doing a lane's work (issue x lane utilisation) of one launch alone, from
+            # the PMC pass of the build traffic_kernel / traffic_build name; for HBM the measured
+            # DRAM fraction
+            if roof["bound"] == "valu":
+                roof["bound_frac"] = roof.get("valu_useful_frac", round(valu_frac, 4))
+                roof["bound_frac_basis"] = ("valu_useful_frac: VALU issue fraction x lane utilisation of one "
+                                            "launch alone (PMC SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU, "
+                                            "GRBM_GUI_ACTIVE; profiles/traffic.json)")
+            else:
+                roof["bound_frac"] = round(hbm_frac, 4)
+                roof["bound_frac_basis"] = "hbm_measured_frac (PMC DRAM bytes per launch)"
+            if tj.get("build"):
+                roof["traffic_build"] = tj["build"]
+                import hashlib
+                with open(vr.LIB_PATH, "rb") as f:
+                    roof["traffic_build_matches"] = tj["build"].endswith(hashlib.sha256(f.read()).hexdigest()[:16])
         else:
             roof["bound"] = "valu" if cfg.store == vr.StorageType.VOXEL_CLUSTER_STORE else "hbm"
             roof["bound_basis"] = "no PMC profile of this config in profiles/traffic.json: by store"
@@ -472,6 +527,15 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            # value / ms_per_step render the SAME view every step, so the learned per-view
+            # orders (work order, lane order) and the crawl-pass skip apply (include/vr.h
+            # vr_forget_orders); the moving view renders every frame from scratch
+            "view": "repeated identical view (learned per-view work/lane orders and crawl skip apply)",
+            "value_moving_view": round(W * H / (ms_moving * 1e-3) / 1e6, 2),
+            "ms_per_step_moving_view": round(ms_moving, 4),
+            "moving_view_basis": "the same pipelined loop, steps frames, the camera eye moved by 1, 2, 3 ulps in "
+                                 "x in turn: no launch sees the view its predecessor or its slot's previous launch "
+                                 "saw, so nothing is learned (every frame a first render, as for a moving camera)",
             "higher_is_better": True,
             "scaling": "strong" if tiling == "fixed" else "weak",
             "vs_baseline": None,
@@ -501,7 +565,7 @@ def main():
             # trace of the same command splits into them: profiles/roofline_phases.py)
             "dispatch_phases": {"warmup": args.warmup, "iso_first": n_iso, "untimed": 40, "iso_grid": n_iso,
                                 "iso_learned": n_iso,
-                                "latency": 5 if grouped else 0, "timed": args.steps},
+                                "latency": 5 if grouped else 0, "timed": args.steps, "moving": args.steps},
         }
         if HW_QUEUES_REQUESTED is not None:
             line["config"]["hw_queues_requested"] = HW_QUEUES_REQUESTED

@@ -272,6 +272,11 @@ typedef enum {
  * so a wrong skip could never shade another frame's pixels).  vr_forget_orders drops what a
  * device has learned, so the next launch renders as a first render (measurement). */
 int vr_forget_orders(int device);
+/* Test hook: the device's next launch skips its crawl pass as if its slot had seen the view
+ * defer nothing.  For the crawl-skip safety net's test only (a launch that then defers a
+ * pixel renders it as 0; the tile pass reports the deferral and the slot stops skipping, so
+ * later launches are exact again).  Never needed by a renderer. */
+int vr_debug_skip_next_crawl(int device);
 /* Every vr_render* call returns VR_E_INVALID on a stream that is capturing a HIP graph
  * (its per-device slot ring and work-order bookkeeping are host state that a graph replay
  * would not repeat). */

@@ -12,6 +12,7 @@
   clock: GRBM_GUI_ACTIVE (sums the 8 XCDs) over the rocprof kernel duration.
   python3 profiles/collect_traffic.py <profile dir> <config> [merge_into.json]"""
 import csv
+import hashlib
 import re
 import glob
 import json
@@ -48,6 +49,10 @@ def main():
            "hbm_bytes_per_launch": int((2 * f_kb + w_kb) * 1024),
            "rocprof_avg_ns": stats.get(kern, {}).get("avg_ns"),
            "kernel_stats": stats}
+    # the library build the passes ran (bench.py compares it with the one it loads)
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "voxelraymarcher_amd", "libvr.so")
+    if os.path.exists(lib):
+        out["build"] = "libvr.so sha256:" + hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
     valu = per_dispatch(os.path.join(root, "pmc_sq"), "SQ_INSTS_VALU").get(kern)
     thr = per_dispatch(os.path.join(root, "pmc_sq"), "SQ_THREAD_CYCLES_VALU").get(kern)
     salu = per_dispatch(os.path.join(root, "pmc_sq"), "SQ_INSTS_SALU").get(kern)

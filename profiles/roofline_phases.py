@@ -5,7 +5,8 @@ recompute every roofline fraction of its JSON line from the trace alone.
   python profiles/roofline_phases.py <run_kernel_trace.csv> <bench_line.json> [out_dir]
 
 bench.py prints `dispatch_phases` -- the number of non-instrumented launches per phase, in
-submission order: warmup, iso_first, untimed, iso_grid, iso_learned, latency (N > 1), timed.
+submission order: warmup, iso_first, untimed, iso_grid, iso_learned, latency (N > 1), timed,
+moving (the pipelined loop with a view that changes every frame).
 Every launch is one tile-pass dispatch (`march_kernel<S, A, false[, HI]>`) followed by one
 crawl-pass dispatch (`crawl_kernel<S, A, false>`) on the same stream, sometimes plus the
 learned orders' builds (`perm_kernel`, `order_kernel`: about every 16th launch of a slot).  Dispatches are taken in
@@ -115,7 +116,7 @@ def main():
         }
     bench = {"iso_first": roof.get("frac"), "iso_grid": roof.get("frac_grid_order"),
              "iso_learned": roof.get("frac_learned_order"),
-             "timed": roof.get("frac_pipelined")}
+             "timed": roof.get("frac_pipelined"), "moving": roof.get("frac_pipelined_moving_view")}
     for ph, fb in bench.items():
         if ph in res["phases"] and fb:
             p = res["phases"][ph]

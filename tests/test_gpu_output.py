@@ -86,3 +86,37 @@ def test_cli_end_to_end(tmp_path, store, algo, flags, lit_kw):
                                                     oracle_lighting_from(lit), W, H, cfg.scale)
     got = decode_png(open(out, "rb").read())
     assert np.array_equal(got, words_to_rgb(want, W, H))
+
+
+@pytest.mark.parametrize("store,algo", [("vcs", "original"), ("hashtable", "longestaxis")])
+def test_cli_gpus_rccl_path(tmp_path, store, algo):
+    """`VoxelRaymarcher ... --gpus 1`: the native multi-GPU host (csrc/cli/multi_gpu.cpp) --
+    the 2-D tile deal per device, RGB8 pack, ncclCommInitAll + ncclGather to device 0, the
+    assembly kernel -- with one rank on this one-GPU box; the PNG equals the oracle's frame."""
+    cfg = vr.CONFIGS["C1"]
+    xyz, rgb = cfg.voxels()
+    scene_path = str(tmp_path / "scene.vox")
+    vr.write_voxel_file(scene_path, xyz, rgb)
+    W, H = 232, 150                        # not a multiple of the 16-pixel tiles: edge blocks
+    out = str(tmp_path / "output.png")
+    r = subprocess.run([EXE, str(cfg.scale), store, algo, "--scene", scene_path, "--width", str(W), "--height", str(H),
+                        "--out", out, "--gpus", "1", "--repeat", "3"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "on 1 GPU(s), tiled + RCCL gather" in r.stdout, r.stdout
+    lit = vr.setup_constant_values()
+    want, _ = oracle.Scene(xyz, rgb, int(vr.parse_storage(store))).render(
+        int(vr.parse_algorithm(algo)), oracle_camera_from(vr.Camera.reference(W, H)), oracle_lighting_from(lit), W, H,
+        cfg.scale)
+    got = decode_png(open(out, "rb").read())
+    assert np.array_equal(got, words_to_rgb(want, W, H))
+
+
+def test_cli_gpus_more_than_visible(tmp_path):
+    """--gpus N above the visible device count is refused before any work (exit 2)."""
+    n = torch.cuda.device_count()
+    r = subprocess.run([EXE, "1", "vcs", "original", "--synth", "64", "--width", "64", "--height", "64",
+                        "--out", str(tmp_path / "o.png"), "--gpus", str(n + 1)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert f"--gpus {n + 1}" in r.stderr and "visible" in r.stderr
+    assert not os.path.exists(tmp_path / "o.png")

@@ -58,6 +58,71 @@ def test_launches_in_flight_on_three_streams(c5_scene, kernel, algo):
     assert torch.equal(last, ref)
 
 
+def test_crawl_skip_safety_net(c5_scene):
+    """The crawl-pass skip's safety net (vr_host.cpp launch, vr_march.hip deferral_report).
+    Every slot first learns a view that defers nothing (C5's top rows: each slot's last crawl
+    pass reports 0).  Then the next launch is forced to skip its crawl pass on C5's crawl rows,
+    as a wrong skip would: its deferred pixels stay 0 (the frame differs).  Its tile pass
+    reports the deferral, so that slot stops skipping: every later launch of the view -- 40,
+    so each of the 16 slots comes round at least twice -- equals the serial frame, and the
+    records the skipped launch left never reach a frame (they carry its launch id).  Without
+    the report the forced slot would skip the crawl pass of this view every 16th launch."""
+    cfg, scene = c5_scene
+    W, H = cfg.width, cfg.height
+    cam, lit = vr.Camera.reference(W, H), vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    algo = vr.RayMarchAlgorithm.ORIGINAL
+    dev = torch.cuda.current_device()
+
+    def frame(r0, r1):
+        out = torch.full(((r1 - r0) * W,), -1, dtype=torch.int32, device="cuda")
+        vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, r0, r1)
+        torch.cuda.synchronize()
+        return out
+
+    vr.forget_orders(dev)
+    quiet = frame(0, 16)
+    for _ in range(40):                          # every slot's crawl pass reports 0 deferrals
+        assert torch.equal(frame(0, 16), quiet)
+    ref = frame(696, 712)
+    assert int((ref == 0).sum()) < ref.numel()
+    vr.debug_skip_next_crawl(dev)
+    skipped = frame(696, 712)
+    assert not torch.equal(skipped, ref), "the forced skip left every deferred pixel shaded"
+    bad = [i for i in range(40) if not torch.equal(frame(696, 712), ref)]
+    assert not bad, f"launches after the forced skip differ from the serial frame: {bad}"
+    assert torch.equal(frame(0, 16), quiet)
+
+
+def test_crawl_skip_key_inputs(c5_scene):
+    """The crawl-pass skip is keyed by everything that decides deferral (vr_host.cpp view_key,
+    crawl_key): one camera and row range, rendered 40 times with TILE and TILE_REWALK
+    alternating on a scene where it defers nothing (the C2 grid: every slot learns to skip),
+    then 40 times on C5's scene, where the same view defers thousands of crawling rays, then
+    on the first scene again.  Every frame equals that scene's serial first render (which
+    test_gpu_parity pins to the oracle): a key without the scene would skip C5's crawl pass."""
+    cfg, c5 = c5_scene
+    c2 = vr.create_scene(*vr.CONFIGS["C2"].voxels(), vr.StorageType.VOXEL_CLUSTER_STORE)
+    W, H, r0, r1 = cfg.width, cfg.height, 696, 712
+    cam, lit = vr.Camera.reference(W, H), vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    algo = vr.RayMarchAlgorithm.ORIGINAL
+    kernels = [vr.Kernel.TILE, vr.Kernel.TILE_REWALK]
+
+    def frame(scene, kernel):
+        out = torch.full(((r1 - r0) * W,), -1, dtype=torch.int32, device="cuda")
+        vr.run_raymarching_kernel(scene, algo, cam, lit, info, W, H, out, r0, r1, kernel=kernel)
+        torch.cuda.synchronize()
+        return out
+
+    vr.forget_orders(torch.cuda.current_device())
+    refs = {id(s): frame(s, vr.Kernel.TILE) for s in (c2, c5)}
+    assert not torch.equal(refs[id(c2)], refs[id(c5)])
+    for scene in (c2, c5, c2):
+        bad = [i for i in range(40) if not torch.equal(frame(scene, kernels[i % 2]), refs[id(scene)])]
+        assert not bad, f"scene {'C5' if scene is c5 else 'C2'}: launches {bad} differ"
+
+
 def test_render_refuses_graph_capture(c5_scene):
     """vr_render* on a stream that is capturing a graph returns VR_E_INVALID before enqueuing
     anything (include/vr.h): the slot ring's event wait/record and the work order's host-side

@@ -95,6 +95,7 @@ SIGNATURES = {
     "vr_tile_buffer_words": (c_uint64, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint32]),
     "vr_deal_stride_default": (c_uint32, [c_uint32]),
     "vr_forget_orders": (c_int, [c_int]),
+    "vr_debug_skip_next_crawl": (c_int, [c_int]),
     "vr_assemble_tiles": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32,
                                   c_uint32, c_void_p]),
     "vr_render_ex": (c_int, [c_void_p, c_int, POINTER(VrCamera), POINTER(VrLighting), POINTER(c_float), c_uint32,

@@ -6,6 +6,9 @@
 //                   [--write-vxb F]   (convert the scene to the .vxb sidecar and exit)
 //                   [--no-shadows] [--point-light X,Y,Z] [--light-dir X,Y,Z] [--light-color R,G,B]
 //                   (the setupConstantValues toggles, Main.cu:26-42, as flags)
+//                   [--gpus N]   (the frame image-tiled over devices 0..N-1 of the node and
+//                                 gathered to device 0 over RCCL: multi_gpu.h; N = 1 takes the
+//                                 same RCCL path with one rank)
 // Defaults follow Main.cu: VCS unless "hashtable", longest axis unless
 // "original" (:45-68), 1920x1080 (:195-196), camera (6,2,6)->(0,0,-1) fov 60
 // (:199), translation 0 (:215), scene file resources/scene.vox (:96-103).
@@ -21,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "multi_gpu.h"
 #include "vr.hpp"
 
 namespace {
@@ -64,7 +68,8 @@ int main(int argc, char* argv[]) {
     std::vector<const char*> pos;
     std::string scene_path = "resources/scene.vox", out_path = "output.png", vxb_path;
     uint32_t width = 1920, height = 1080, synth = 0;
-    int device = 0, repeat = 1;
+    int device = 0, repeat = 1, gpus = 0;
+    bool multi = false;                      // --gpus given: the RCCL-tiled frame
     bool shadows = true, point_light = false, has_dir = false;
     float light_pos[3] = {10.0f, 10.0f, -10.0f}, light_dir[3] = {1.0f, 1.0f, 1.0f}, light_color[3] = {1.0f, 1.0f, 1.0f};
     auto vec3 = [](const char* name, const char* v, float out[3]) {
@@ -82,6 +87,7 @@ int main(int argc, char* argv[]) {
         else if (a == "--height") height = (uint32_t)std::strtoul(next("--height"), nullptr, 10);
         else if (a == "--device") device = std::atoi(next("--device"));
         else if (a == "--synth") synth = (uint32_t)std::strtoul(next("--synth"), nullptr, 10);
+        else if (a == "--gpus") { multi = true; gpus = std::atoi(next("--gpus")); }
         else if (a == "--repeat") repeat = std::max(1, std::atoi(next("--repeat")));
         else if (a == "--write-vxb") vxb_path = next("--write-vxb");
         else if (a == "--no-shadows") shadows = false;
@@ -91,7 +97,7 @@ int main(int argc, char* argv[]) {
         else if (a == "-h" || a == "--help") {
             std::cout << "usage: VoxelRaymarcher [scale] {hashtable|vcs} {original|longestaxis} [--scene F] "
                          "[--width W] [--height H] [--out F] [--device N] [--synth N] [--repeat K] [--write-vxb F] "
-                         "[--no-shadows] [--point-light X,Y,Z] [--light-dir X,Y,Z] [--light-color R,G,B]" << std::endl;
+                         "[--no-shadows] [--point-light X,Y,Z] [--light-dir X,Y,Z] [--light-color R,G,B] [--gpus N]" << std::endl;
             return 0;
         } else pos.push_back(argv[i]);
     }
@@ -132,6 +138,11 @@ int main(int argc, char* argv[]) {
     HIP_OK(hipGetDeviceCount(&ndev));
     std::printf("Device Count: %d\n", ndev);                   // pickCudaDevice (:82-94)
     if (device >= ndev) { std::cerr << "no such device" << std::endl; return 1; }
+    if (multi && (gpus < 1 || gpus > ndev)) {
+        std::cerr << "ERROR: --gpus " << gpus << ": " << ndev << " HIP device(s) visible (need 1.." << ndev << ")"
+                  << std::endl;
+        return 2;
+    }
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device));
     std::printf("Device: %s (%s)\n", prop.name, prop.gcnArchName);
@@ -167,6 +178,41 @@ int main(int argc, char* argv[]) {
         lit.use_point_light = point_light;                       // Main.cu:37
         lit.use_shadows = shadows;                               // Main.cu:40
 
+        if (multi) {
+            // The frame image-tiled over devices 0..gpus-1, RCCL-gathered to device 0 (multi_gpu.h)
+            vrx::MultiGpuFrame mg;
+            if (!mg.init(gpus, (vr_store)store, cpu.coords(), cpu.colors(), width, height)) {
+                std::cerr << "ERROR: " << mg.error() << std::endl;
+                return 1;
+            }
+            const float t[3] = {sinfo.translationVector.x, sinfo.translationVector.y, sinfo.translationVector.z};
+            vrx::MultiGpuTiming best, tm;
+            best.frame_ms = 1e30;
+            for (int r = 0; r < repeat; ++r) {
+                if (!mg.render((vr_algo)algo, camera.raw(), lit, t, sinfo.scale, &tm)) {
+                    std::cerr << "ERROR: " << mg.error() << std::endl;
+                    return 1;
+                }
+                if (tm.frame_ms < best.frame_ms) best = tm;
+            }
+            std::cout << "Execution Time for Ray Marching Algorithm is: " << (long long)(best.frame_ms * 1000.0)
+                      << " microseconds on " << gpus << " GPU(s), tiled + RCCL gather + assembly ("
+                      << (double)width * height / (best.frame_ms * 1e3) << " Mrays/s)" << std::endl;
+            for (size_t i = 0; i < best.rank_render_ms.size(); ++i)
+                std::cout << "  rank " << i << " render " << (long long)(best.rank_render_ms[i] * 1000.0f)
+                          << " microseconds" << std::endl;
+            std::vector<uint8_t> host;
+            if (!mg.download(host)) {
+                std::cerr << "ERROR: " << mg.error() << std::endl;
+                return 1;
+            }
+            if (vr_png_write(out_path.c_str(), host.data(), width, height, 3, 6) != VR_OK) {
+                std::cerr << "ERROR: Failed to write image to: " << out_path << " (" << vr_last_error() << ")" << std::endl;
+                return 1;
+            }
+            std::cout << "Wrote " << out_path << std::endl;
+            return 0;
+        }
         uint32_t* fb = nullptr;
         uint8_t* rgb = nullptr;
         HIP_OK(hipMalloc(&fb, (size_t)width * height * 4));

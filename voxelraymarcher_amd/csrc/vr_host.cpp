@@ -586,6 +586,7 @@ struct SlotRing {
         hipStream_t last_stream = nullptr;
         uint32_t last_idx = 0;
         uint64_t last_key = 0;             // the view of the device's previous launch
+        bool force_skip = false;           // vr_debug_skip_next_crawl (tests)
     } dev[64];
     SlotRing(const char* n, size_t w, uint32_t s) : name(n), words(w), nslots(s) {}
 };
@@ -731,10 +732,16 @@ bool order_enabled() {
     return on;
 }
 
-// The view a launch renders, for the learned orders: an FNV-1a hash of the scene, the
-// algorithm and every value field of the view (camera, lights, transform, frame size, the
-// launch's rows and its band / tile deal; make_view zeroes the struct, so its padding is 0).
-// The per-launch buffers (out and after) are not part of it.
+// The view a launch renders, for the learned orders and the crawl-pass skip: an FNV-1a hash
+// of the scene (its per-process serial), the algorithm and every value field of the view --
+// the KView prefix above `out`: camera (llc, hor, ver, org), lights (L, LC, LP and the
+// host-made Lr, L_fast, Lw, L_order, L_cls, L_unit, L_eq), transform (translation, scale_f),
+// use_point_light, use_shadows, frame size (W, H), the launch's rows (row0, band_rows, rank,
+// nranks, local_rows, row_limit, band_minv) and its tile deal (LW, tile_cols, tile_minv,
+// col_R, col_rank, col_stride).  make_view zeroes the struct, so its padding is 0.  These,
+// with the compile-time tile budget (vr::kTileBudget), are every input of which pixels the
+// tile pass defers (vr_internal.h KView: a field added after `out` fails a static_assert
+// until reviewed).  The per-launch buffers (out and after) are not part of it.
 uint64_t view_key(const vr_scene* s, vr_algo algo, const vr::KView& v) {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](const void* p, size_t n) {
@@ -746,6 +753,17 @@ uint64_t view_key(const vr_scene* s, vr_algo algo, const vr::KView& v) {
     mix(&a, sizeof a);
     mix(&v, offsetof(vr::KView, out));
     return h;
+}
+
+// The crawl-pass skip's key: the view, plus the per-launch knobs that change how the crawl
+// pass resumes deferred pixels (the list's capacity, walk-from-the-start records).  Which
+// pixels defer is a function of the view alone: the tile pass's budget is compile-time
+// (vr::kTileBudget) and everything else it reads is in the view (vr_internal.h KView).
+uint64_t crawl_key(uint64_t key, const vr::KView& v) {
+    const uint32_t knobs[2] = {v.defer_cap, v.crawl_rewalk};
+    const unsigned char* b = (const unsigned char*)knobs;
+    for (size_t i = 0; i < sizeof knobs; ++i) key = (key ^ b[i]) * 1099511628211ull;
+    return key;
 }
 
 int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, uint32_t occupancy, vr::KView& v,
@@ -773,6 +791,12 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     SlotLease lease;
     int rc = lease.acquire(g_defer_ring, s->device, st);
     if (rc) return rc;
+    // An error after the slot was taken: the slot's event is recorded again on `st` first (a
+    // stream-ordered free of its old buffers may already be queued there), then the error.
+    auto bail = [&](hipError_t e, const char* what) {
+        (void)lease.release(st);
+        return hip_fail(e, what);
+    };
     v.defer = lease.p;
     v.defer_cap = (v.defer_cap && v.defer_cap < vr::kDeferCap) ? v.defer_cap : vr::kDeferCap;
     v.defer_stat = lease.D().stat_dev;
@@ -828,7 +852,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
                 if (O.order) (void)hipFreeAsync(O.order, st);
                 O.cost = nullptr;
                 O.order = nullptr;
-                return hip_fail(e, "work order buffers");
+                return bail(e, "work order buffers");
             }
             O.cap = n;
         }
@@ -855,7 +879,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
             if (e == hipSuccess) e = hipMallocAsync((void**)&O.perm, nperm, st);
             if (e != hipSuccess) {
                 O.perm = nullptr;
-                return hip_fail(e, "lane order buffer");
+                return bail(e, "lane order buffer");
             }
             O.bcap = nperm;
         }
@@ -866,7 +890,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
             // 4 B per pixel, only between this launch's tile pass and its perm_kernel (freed
             // stream-ordered after it): the slots keep 1 B per pixel each, not 5
             const hipError_t e = hipMallocAsync((void**)&pcost, sizeof(uint32_t) * npx, st);
-            if (e != hipSuccess) return hip_fail(e, "lane order walk lengths");
+            if (e != hipSuccess) return bail(e, "lane order walk lengths");
         }
         v.pcost = pcost;
     }
@@ -876,22 +900,40 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // so even a wrong skip cannot put another frame's pixels into a frame; the records it
     // leaves raise the count the next crawl pass of the slot reports, which ends the skipping.
     // (C2 lone launch: the 4-us empty crawl pass and a kernel boundary.)
+    //   The safety net: every tile pass that defers a pixel writes {launch id, 1}
+    // into the slot's report word (vr_march.hip deferral_report), skipped launches included.
+    // While the slot skips, nothing else writes that word (its last crawl pass left
+    // {id, 0}), so a nonzero count there means a skipped launch deferred: the skipping ends,
+    // and the slot's next launch runs the crawl pass, which drops the stale records (they
+    // carry another launch's id) and resets the list.  What the net cannot repair is the
+    // frames of the skipped launches that deferred before the host saw the report (their
+    // deferred pixels stay 0): that needs a deferral that is not a function of the crawl key
+    // below, which the kernels do not have (vr_internal.h KView, "end of the view's
+    // identity"); tests/test_gpu_slots.py forces one (vr_debug_skip_next_crawl) to test the net.
     bool crawl = true;
     {
         uint32_t lid = ++D.launch_serial;
         if (lid == 0u) lid = ++D.launch_serial;
         v.launch_id = lid;
-        if (O.ckey != key) {
+        const uint64_t ckey = crawl_key(key, v);
+        const uint64_t r = *reinterpret_cast<volatile uint64_t*>(D.stat_host + 2 + 2 * (size_t)lease.idx);
+        if (O.ckey != ckey) {
             O.czero = false;
-        } else if (!O.czero && O.cid != 0u) {
-            const uint64_t r = *reinterpret_cast<volatile uint64_t*>(D.stat_host + 2 + 2 * (size_t)lease.idx);
+        } else if (O.czero) {
+            if ((uint32_t)(r >> 32) != 0u) O.czero = false;   // a skipped launch deferred
+        } else if (O.cid != 0u) {
             O.czero = (uint32_t)r == O.cid && (uint32_t)(r >> 32) == 0u;
         }
+        if (D.force_skip) {                    // (vr_debug_skip_next_crawl: tests of the net)
+            D.force_skip = false;
+            O.czero = true;
+            O.ckey = ckey;
+        }
         crawl = !(O.czero && crawl_skip_enabled());
+        v.slot_stat = D.stat_dev + 2 + 2 * (size_t)lease.idx;
         if (crawl) {
-            v.slot_stat = D.stat_dev + 2 + 2 * (size_t)lease.idx;
             O.cid = lid;
-            O.ckey = key;
+            O.ckey = ckey;
         }
     }
     // crawl pass grid from the records an earlier launch deferred (a hint: any grid renders
@@ -1343,6 +1385,14 @@ int vr_forget_orders(int device) {
         O.cid = 0;
     }
     D.last_key = 0;
+    return VR_OK;
+}
+
+int vr_debug_skip_next_crawl(int device) {
+    if (device < 0 || device >= 64) return fail(VR_E_INVALID, "device index out of range");
+    SlotRing::Dev& D = g_defer_ring.dev[device];
+    std::lock_guard<std::mutex> lk(D.mu);
+    D.force_skip = true;
     return VR_OK;
 }
 

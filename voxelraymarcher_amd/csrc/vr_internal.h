@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include <string>
@@ -112,6 +113,13 @@ struct KView {
     uint32_t tile_cols;       // 0: whole rows (no column deal)
     uint32_t tile_minv;       // floor(2^32 / tile_cols) (2^32 - 1 for 1)
     uint32_t col_R, col_rank, col_stride;   // 2-D deal: ranks, this rank, stride (< col_R)
+    // ---- end of the view's identity.  Everything above `out` is hashed, with the scene and
+    // the algorithm, into the view key (vr_host.cpp view_key) under which the learned orders
+    // and the crawl-pass skip are kept: a field that changes any pixel, or which pixels the
+    // tile pass defers to the crawl pass, MUST sit above this line.  Everything below is a
+    // per-launch buffer or a launch knob that changes neither (checked by the static_assert
+    // after the struct: adding a field below fails the build until it is reviewed here).
+    // (The deferral's other inputs are compile-time: kTileBudget, and the walk itself.)
     uint32_t* out;
     unsigned long long* bytes;
     // (COUNT launches, optional) [0] crawl iterations the crawl pass fast-forwarded in
@@ -137,10 +145,19 @@ struct KView {
     const uint8_t* perm;
     uint32_t* pcost;
     // (or null) the launch slot's host-mapped crawl report: the crawl pass writes
-    // {launch_id, records deferred} there in one 8-B store (the host's crawl-pass skip)
+    // {launch_id, records deferred} there in one 8-B store (the host's crawl-pass skip);
+    // a tile pass that defers a pixel writes {launch_id, 1} there first (deferral_report:
+    // on a launch whose crawl pass the host skipped, the report ends the skipping)
     uint32_t* slot_stat;
     uint32_t launch_id;
 };
+// The per-launch tail of KView (see "end of the view's identity" above): out, bytes, stats,
+// defer, defer_cap, crawl_rewalk, crawl_rpw, defer_stat, order, cost, perm, pcost, slot_stat,
+// launch_id.  defer_cap and crawl_rewalk change only how deferred pixels are resumed, never
+// which ones defer; the crawl-pass skip keys them anyway (vr_host.cpp crawl_key).
+// (10 pointers, 4 words, padding: 104 bytes)
+static_assert(sizeof(KView) - offsetof(KView, out) == 104,
+              "a KView field was added after `out`: review whether it belongs to the view identity");
 
 // Rays that start a cluster-skip crawl (see vr_march.hip crawl_steps) in the
 // tile pass, and pixels that exceed kTileBudget, are deferred to a second pass

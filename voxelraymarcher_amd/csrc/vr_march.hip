@@ -267,6 +267,16 @@ constexpr uint32_t kTilesX = VR_TILES_X, kTilesY = VR_TILES_Y;
 // in grid_original_rt): the pixel is the crawl pass's already.
 constexpr uint32_t kDeferredIters = 0xFFFFFFFFu;
 
+// A tile-pass lane that defers its pixel tells the host, through the launch slot's
+// host-mapped report word (KView::slot_stat): {launch id, 1}.  On a launch that runs its
+// crawl pass the pass overwrites it with its own count.  On a launch whose crawl pass the
+// host skipped -- believing the view defers nothing -- it is the only writer, and the host
+// stops skipping when it sees it (vr_host.cpp launch): the next launch of the slot runs the
+// crawl pass, which drops the stale records and resets the list.  (Rare: one 8-B store.)
+__device__ __forceinline__ void deferral_report(const KView& v) {
+    if (v.slot_stat) *reinterpret_cast<uint2*>(v.slot_stat) = uint2{v.launch_id, 1u};
+}
+
 // The tile group (column, row of kTilesX x kTilesY tiles) this tile-pass workgroup
 // renders: the work order's entry (heaviest first, KView::order), or its grid position
 // (a uniform load: SGPRs).
@@ -695,6 +705,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                     // free (unwinds like an abort); otherwise walk on plainly.
                     if ((kx || ky || kz) && v.defer) {
                         const uint32_t idx = atomicAdd(v.defer, 1u);
+                        deferral_report(v);
                         if (idx < v.defer_cap) {
                             // (the tile pass writes this pixel as 0; the crawl pass,
                             // which runs after it, overwrites it and counts its bytes)
@@ -1540,6 +1551,7 @@ __device__ __forceinline__ uint32_t light_and_shadow(Walker<STORE, COUNT, CRAWL>
 // pixel by the marker).
 __device__ __forceinline__ uint32_t defer_rewalk(const KView& v) {
     const uint32_t idx = atomicAdd(v.defer, 1u);
+    deferral_report(v);
     if (idx < v.defer_cap) {
         uint32_t* r = v.defer + 4 + (size_t)idx * kDeferRecWords;
         r[0] = tile_pixels()[threadIdx.x];

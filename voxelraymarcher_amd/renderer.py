@@ -377,6 +377,12 @@ def forget_orders(device: int = 0) -> None:
     check(lib().vr_forget_orders(int(device)), "vr_forget_orders")
 
 
+def debug_skip_next_crawl(device: int = 0) -> None:
+    """Test hook (vr_debug_skip_next_crawl): the device's next launch skips its crawl pass as
+    if its slot had seen the view defer nothing -- for the test of the crawl-skip safety net."""
+    check(lib().vr_debug_skip_next_crawl(int(device)), "vr_debug_skip_next_crawl")
+
+
 def render_tiles(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, lighting: _capi.VrLighting,
                  info: VoxelSceneInfo, width: int, height: int, band_rows: int, tile_cols: int, rank: int,
                  nranks: int, out: torch.Tensor, stream=None) -> torch.Tensor:
