@@ -77,15 +77,13 @@ def test_device_build_errors():
 def test_vcs_region_limit(build):
     """VCS walks address cluster masks by a 32-bit byte offset (64 KB per occupied
     region): a VCS scene may hold at most 65 536 occupied regions; more is an error.
-    The hash store has the same bound since round 5 (its key-presence filter is 32 KB per
-    occupied region, addressed the same way)."""
+    (The hash store has no bound -- test_hash_scene_past_the_vcs_bound.)"""
     g = np.arange(41, dtype=np.int32) * 64
     xyz = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)   # 68 921 regions
     rgb = np.full(len(xyz), 7, np.uint32)
-    for store in (vr.StorageType.VOXEL_CLUSTER_STORE, vr.StorageType.HASH_TABLE):
-        with pytest.raises(vr.VrError) as e:
-            vr.create_scene(xyz, rgb, store, build=build)
-        assert e.value.code == -1 and "65536" in str(e.value)
+    with pytest.raises(vr.VrError) as e:
+        vr.create_scene(xyz, rgb, vr.StorageType.VOXEL_CLUSTER_STORE, build=build)
+    assert e.value.code == -1 and "65536" in str(e.value)
     if build != vr.Build.DEVICE:
         return
     # the largest allowed scene (4 GB of masks) builds -- when the device has room for it
@@ -122,6 +120,41 @@ def test_vcs_region_limit(build):
         assert np.array_equal(got, want) and gb == wb
         assert np.count_nonzero(want) > 0
     okh.close()
+
+
+@pytest.mark.parametrize("build", [vr.Build.DEVICE, vr.Build.HOST], ids=["device", "host"])
+def test_hash_scene_past_the_vcs_bound(build):
+    """The cuckoo store has no region bound (as the reference's CuckooHashTable per region):
+    52^3 = 140 608 occupied regions, one voxel each, so the key-presence filter (32 KB per
+    region) runs past 4 GB and the last regions' filter words lie beyond any 32-bit offset.
+    A camera in the region of largest id sees its voxel exactly as the oracle does (pixels
+    and algorithmic bytes), both algorithms, both builders."""
+    import torch
+
+    import oracle
+    from tests.helpers import gpu_render, oracle_camera_from, oracle_lighting_from
+    free, _ = torch.cuda.mem_get_info()
+    if free < 16 * (1 << 30):
+        pytest.skip(f"{free >> 30} GiB free: the 140 608-region hash scene needs ~6 GiB")
+    D = 52
+    g = np.arange(D, dtype=np.int32) * 64
+    xyz = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3) + 5
+    rgb = (np.arange(len(xyz), dtype=np.uint32) * 2654435761 & 0xFFFFFF).astype(np.uint32)
+    scene = vr.create_scene(xyz, rgb, vr.StorageType.HASH_TABLE, build=build)
+    assert scene.info()["region_count"] == D ** 3 > 131072
+    rid = (xyz[:, 0] // 64) + (xyz[:, 1] // 64) * D + (xyz[:, 2] // 64) * D * D
+    corner = xyz[int(np.argmax(rid))].astype(float)
+    cam = vr.Camera(tuple(corner + 20.0), tuple(corner), (0.0, 1.0, 0.0), 20.0, 1.0)
+    lit = vr.setup_constant_values()
+    ref = oracle.Scene(xyz, rgb, 1)
+    for algo in (vr.RayMarchAlgorithm.ORIGINAL, vr.RayMarchAlgorithm.LONGEST_AXIS):
+        want, wb = ref.render(int(algo), oracle_camera_from(cam), oracle_lighting_from(lit), 16, 16, 1)
+        got, gb = gpu_render(scene, algo, cam, lit, vr.VoxelSceneInfo((0.0, 0.0, 0.0), 1), 16, 16, count=True)
+        assert np.array_equal(got, want) and gb == wb
+        assert np.count_nonzero(want) > 0          # the last region's voxel is hit
+        got2, _ = gpu_render(scene, algo, cam, lit, vr.VoxelSceneInfo((0.0, 0.0, 0.0), 1), 16, 16)
+        assert np.array_equal(got2, want)
+    scene.close()
 
 
 def test_device_built_scene_renders_like_oracle():

@@ -372,9 +372,9 @@ int build_scene_gpu(int store, const int32_t* xyz, const uint32_t* rgb, uint64_t
     }
     out.n_regions = nr;
     out.n_voxels = m;
-    if (nr > kVcsMaxRegions) {
-        err = std::string(store == STORE_VCS ? "VCS" : "hashtable") + " scene with " + std::to_string(nr) +
-              " occupied 64^3 regions (at most " + std::to_string(kVcsMaxRegions) + ")";
+    if (store == STORE_VCS && nr > kVcsMaxRegions) {   // (cuckoo scenes have no region bound)
+        err = "VCS scene with " + std::to_string(nr) + " occupied 64^3 regions (at most " +
+              std::to_string(kVcsMaxRegions) + ")";
         return -1;
     }
 

@@ -253,10 +253,19 @@ struct Ctx {
     // so a cluster's 16 words are contiguous (one 128-B record, in-cluster
     // word w = (x&7)<<1 | y2 as before) and the index of an in-region voxel
     // is a few bit operations.
-    __device__ __forceinline__ const uint2* masks(uint32_t reg, int32_t cid) const {
+    __device__ __forceinline__ static uint32_t slot_of(int32_t cid) {
         const uint32_t c = (uint32_t)cid;
-        const uint32_t slot = (c >> 6) | (((c >> 3) & 7u) << 3) | ((c & 7u) << 6);
-        return s.vcs_mask + (size_t)reg * 8192u + (slot << 4);
+        return (c >> 6) | (((c >> 3) & 7u) << 3) | ((c & 7u) << 6);
+    }
+    __device__ __forceinline__ const uint2* masks(uint32_t reg, int32_t cid) const {
+        return s.vcs_mask + (size_t)reg * 8192u + (slot_of(cid) << 4);
+    }
+    // Word w of cluster slot `slot`'s record in region reg, addressed as a 32-bit byte offset
+    // from the scene's (uniform) mask array, as the walks' own loads are: no 64-bit per-region
+    // pointer is made (one that is, is loop-invariant, hoisted out of the walks and spilled).
+    __device__ __forceinline__ Blk mword(uint32_t reg, uint32_t slot, uint32_t w) const {
+        return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(s.vcs_mask) +
+                                               ((reg << 16) | (slot << 7) | (w << 3)));
     }
     __device__ __forceinline__ static uint32_t word_index(uint32_t x, uint32_t y, uint32_t z) {   // x,y,z < 64
         // v_bfe + 3 v_lshl_or; the two v_and (y & 0x38, z & 0x38) are shared
@@ -289,7 +298,7 @@ struct Ctx {
     __device__ __forceinline__ Blk mask_word(uint32_t reg, int32_t x, int32_t y, int32_t z) const {
         const int32_t cid = cluster_id(x, y, z);
         if (cid < 0) return Blk{0u, kNone};
-        return masks(reg, cid)[in_cluster(x, y, z) >> 5];
+        return mword(reg, slot_of(cid), in_cluster(x, y, z) >> 5);
     }
 
     // Reference binary-search probes for a key of rank `rank` (number of keys
@@ -320,7 +329,7 @@ struct Ctx {
     // full key is >= K (found iff that key equals K and is present).  Exact, rare.
     __device__ __forceinline__ uint32_t lookup_aliased(uint32_t reg, int32_t x, int32_t y, int32_t z) {
         const int32_t cid = cluster_id(x, y, z);
-        const uint2* m = masks(reg, cid);
+        const uint32_t slot = slot_of(cid);
         const uint32_t K = ((uint32_t)x << 20) | ((uint32_t)y << 10) | (uint32_t)z;
         const uint32_t bx = ((uint32_t)cid >> 6) * 8u, by = (((uint32_t)cid >> 3) & 7u) * 8u, bz = ((uint32_t)cid & 7u) * 8u;
         auto full = [&](uint32_t q) { return ((bx + (q >> 6)) << 20) | ((by + ((q >> 3) & 7u)) << 10) | (bz + (q & 7u)); };
@@ -330,15 +339,17 @@ struct Ctx {
             if (full(mid) < K) lo = mid + 1; else hi = mid;
         }
         if (lo == 512u) {
-            const uint2 m15 = m[15];
-            count_bsearch(m, m15.y + __popc(m15.x), false);
+            if (COUNT) {
+                const uint2 m15 = mword(reg, slot, 15u);
+                count_bsearch(masks(reg, cid), m15.y + __popc(m15.x), false);
+            }
             return kEmpty;
         }
-        const uint2 w = m[lo >> 5];
+        const uint2 w = mword(reg, slot, lo >> 5);
         const uint32_t bit = lo & 31u;
         const bool found = full(lo) == K && ((w.x >> bit) & 1u);
         const uint32_t idx = w.y + __popc(w.x & ((1u << bit) - 1u));
-        count_bsearch(m, idx, found);
+        if (COUNT) count_bsearch(masks(reg, cid), idx, found);
         return found ? s.vcs_vals[idx] : kEmpty;
     }
 

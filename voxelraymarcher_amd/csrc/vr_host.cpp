@@ -251,9 +251,8 @@ int build_scene_host(int device, vr_store store, const int32_t* xyz, const uint3
         }
     const uint32_t nr = (uint32_t)region_begin.size();
     region_begin.push_back(m);
-    if (nr > vr::kVcsMaxRegions)
-        return fail(VR_E_INVALID, std::string(store == VR_STORE_VCS ? "VCS" : "hashtable") + " scene with " +
-                                      std::to_string(nr) + " occupied 64^3 regions (at most " +
+    if (store == VR_STORE_VCS && nr > vr::kVcsMaxRegions)     // (cuckoo scenes have no region bound)
+        return fail(VR_E_INVALID, "VCS scene with " + std::to_string(nr) + " occupied 64^3 regions (at most " +
                                       std::to_string(vr::kVcsMaxRegions) + ")");
 
     vr_scene* s = new vr_scene();

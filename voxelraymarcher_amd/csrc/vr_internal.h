@@ -34,9 +34,9 @@ constexpr uint32_t kCrawlBudget = 1u << 30;
 constexpr uint32_t kDeferMarker = 0xFFFFFFFFu;
 // VCS walks address a region's cluster masks as a 32-bit byte offset from the
 // scene's mask array (64 KB per occupied 64^3 region): at most 65536 occupied
-// regions (4 GB of masks) per VCS scene; the builders reject larger scenes.  The
-// same bound holds for cuckoo scenes, whose key-presence filter is 32 KB per
-// occupied region (2 GB at the bound, addressed the same way).
+// regions (4 GB of masks) per VCS scene; the builders reject larger scenes.  Cuckoo
+// scenes have no such bound (as the reference's): their key-presence filter (32 KB per
+// occupied region) is addressed with 64-bit offsets.
 constexpr uint32_t kVcsMaxRegions = 65536u;
 // words of a cuckoo region's key-presence filter (64^3 bits)
 constexpr uint32_t kHashFilterWords = 8192u;

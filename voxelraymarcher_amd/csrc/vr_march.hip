@@ -365,6 +365,11 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
     // kernel runs at its 72-VGPR limit and the longer-lived values cost spills
     // there (C2 +1.6 %, C3 +4 %), so VCS keeps the plain divisions.
     static constexpr bool kFastSetup = STORE == STORE_HASH;
+    // VR_LONG_REMAT (the VCS longest-axis tile pass): see primary_regions
+#ifndef VR_LONG_REMAT
+#define VR_LONG_REMAT 1
+#endif
+    static constexpr bool kRematDir = VR_LONG_REMAT && STORE == STORE_VCS && !CRAWL;
     // what a deferred crawl must know to be resumed (see the deferral below):
     // bit 1 = the shadow walk is the longest-axis one; the lit colour of the hit
     uint32_t ctx = 0, lit_saved = 0;
@@ -780,14 +785,14 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             // no cluster skips here: with every lane's direction in div_fast's domain no
             // numerator (a voxel plane's, >= ~EPSILON/2 from o) leaves it -- no check at all
             const bool okw = __builtin_amdgcn_ballot_w64(!walk_ok) == 0;
-            // the region's filter words as a 32-bit byte offset from the scene's (SGPR-base loads)
-            const uint32_t foff = reg << 15;
+            // the region's filter words (64-bit: a cuckoo scene has no region bound, vr_internal.h)
+            const uint32_t* freg = s.ht_filter + (size_t)reg * kHashFilterWords;
             uint32_t fw = 0, bit = 0;
             uint32_t ic = this->iters + (0x42800000u - kBudget);   // biased count (see the VCS walk)
             for (;;) {
                 const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
                 const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
-                fw = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s.ht_filter) + (foff | (wi << 2)));
+                fw = freg[wi];
                 __builtin_amdgcn_sched_barrier(0);   // issue the load before the step
                 // rayMarchVoxelGrid's voxel step (Renderer.cuh:318-331), while the word loads
                 const float ax = next_plane_fma(o.x, gx, ex) - o.x, ay = next_plane_fma(o.y, gy, ey) - o.y,
@@ -834,15 +839,23 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
                 if (this->in_region_bits_nz(o)) aborted = true;    // budget spent inside the region
                 return false;
             }
-            // the hit (o unstepped: the probed voxel): CuckooHashTable::lookupVoxel's two probes
-            const uint32_t key = lshl_or(lshl_or((uint32_t)f2i(o.x), 10u, (uint32_t)f2i(o.y)), 10u, (uint32_t)f2i(o.z));
-            const uint4 m = s.ht_meta[reg];        // {base, M, prime, offset}
-            const uint2* t1 = s.ht_slots + m.x;
-            const uint2 e1 = t1[hash1(key, m.w) % m.y];
-            const uint2 e2 = t1[m.y + hash2(key, m.z) % m.y];
-            const bool m1 = e1.x == key;
-            this->count(m1 ? 0u : 4u);             // key1 + val1 (8, counted above), or key1 + key2 + val2
-            col = m1 ? e1.y : e2.y;
+            // A shadow walk's hit needs no value: the reference's lookup returns the voxel's
+            // colour, and a shadow walk only asks whether it is EMPTY_VAL -- which no stored colour
+            // is (< 2^24) -- so the set filter bit (the tables' exact key set) already answers
+            // it.  The two random table reads (HBM for C4's 400-MB store) are skipped; the COUNT
+            // build still makes them, for the bytes the reference reads (8 or 12).
+            col = 0u;                              // (a shadow walk's hit: any colour but EMPTY_VAL)
+            if (!SHADOW || COUNT) {
+                // the hit (o unstepped: the probed voxel): CuckooHashTable::lookupVoxel's two probes
+                const uint32_t key = lshl_or(lshl_or((uint32_t)f2i(o.x), 10u, (uint32_t)f2i(o.y)), 10u, (uint32_t)f2i(o.z));
+                const uint4 m = s.ht_meta[reg];    // {base, M, prime, offset}
+                const uint2* t1 = s.ht_slots + m.x;
+                const uint2 e1 = t1[hash1(key, m.w) % m.y];
+                const uint2 e2 = t1[m.y + hash2(key, m.z) % m.y];
+                const bool m1 = e1.x == key;
+                this->count(m1 ? 0u : 4u);         // key1 + val1 (8, counted above), or key1 + key2 + val2
+                col = m1 ? e1.y : e2.y;
+            }
         }
         if (col == kEmpty) return false;
         if (!SHADOW) {
@@ -1418,6 +1431,11 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
         }
         auto cyc = this->cycle_start(cr, o);
         while (in_scene(cr)) {
+            // (VCS longest axis: the direction is made opaque per region round, so the walk's
+            // per-direction values -- longest-axis frame, sign classes, the tail's plane signs --
+            // are made inside the round instead of hoisted out of it and kept live through every
+            // walk, which spilled them: VR_LONG_REMAT)
+            if (kRematDir && ALGO == ALGO_LONGEST) asm volatile("" : "+v"(d.x), "+v"(d.y), "+v"(d.z));
             if (!tick()) return false;
             VR_DIAG_COUNT(10);                         // primary region rounds
             uint32_t reg = region_at(cr);
@@ -1458,6 +1476,7 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
         }
         auto cyc = this->cycle_start(cr, o);
         while (in_scene(cr)) {
+            if (kRematDir && LONGEST) asm volatile("" : "+s"(d.x), "+s"(d.y), "+s"(d.z));   // (see primary_regions; uniform)
             if (!tick()) return false;
             VR_DIAG_COUNT(12);                         // shadow region rounds
             uint32_t reg = region_at(cr);
@@ -1684,8 +1703,12 @@ __device__ __forceinline__ void add_ff(const KView& v, uint32_t lane, unsigned l
 // and the longest-axis walk (C3 0.2311 -> 0.2289 per frame, 0.2815 -> 0.2862 alone),
 // profiles/r04/ab_orig_waves_C4.txt, ab_long_waves_C3.txt.  The host picks HI for a launch
 // whose device is still running another stream's (the AUTO schedule's test).
+// (Round 6: 7 for the cuckoo walk too.  Since its shadow walks answer a hit from the filter
+// alone -- no table reads -- the 8-wave variant's SGPRs spill into VGPR lanes, 16 v_readlane
+// per loop iteration: C4 per frame in flight 0.0500 -> 0.0746 ms at 8 waves, 0.0466 at 7,
+// profiles/r06/ab_C4_*.txt.)
 #ifndef VR_ORIG_WAVES_HI
-#define VR_ORIG_WAVES_HI 8
+#define VR_ORIG_WAVES_HI 7
 #endif
 #ifndef VR_LONG_WAVES_HI
 #define VR_LONG_WAVES_HI 7
@@ -2099,10 +2122,14 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
 #ifdef VR_ISA_ONLY
     // ISA-inspection builds (csrc/Makefile isa1, profiles/loop_isa.py): one kernel pair
     // only, e.g. -DVR_ISA_ONLY=ALGO_LONGEST for the VCS longest-axis tile pass; never a library
-    (void)algo; (void)count; (void)store;
-    VR_LAUNCH(STORE_VCS, VR_ISA_ONLY, false);
-    return hipGetLastError();
+    // (-DVR_ISA_STORE=STORE_HASH for a cuckoo pair, with its in-flight variant)
+#ifndef VR_ISA_STORE
+#define VR_ISA_STORE STORE_VCS
 #endif
+    (void)algo; (void)count; (void)store;
+    if (in_flight) VR_LAUNCH_HI(VR_ISA_STORE, VR_ISA_ONLY, false, true);
+    else VR_LAUNCH(VR_ISA_STORE, VR_ISA_ONLY, false);
+#else
     // (the in-flight occupancy variants exist for the uninstrumented cuckoo original and
     // VCS longest-axis walks; the VCS original walk is fastest at 7 waves either way)
     const bool hi = in_flight && !count;
@@ -2118,6 +2145,7 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
         }
         else { if (count) VR_LAUNCH(STORE_HASH, ALGO_LONGEST, true); else VR_LAUNCH(STORE_HASH, ALGO_LONGEST, false); }
     }
+#endif
 #undef VR_LAUNCH
 #undef VR_LAUNCH_HI
     return hipGetLastError();
