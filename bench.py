@@ -7,10 +7,12 @@ roofline of the dominant kernel and the CPU oracle baseline.
                   [--tiling auto|weak|fixed]
 
 A step = one full frame.  With N > 1 ranks the frame is dealt over the ranks --
-fixed tiling: the 2-D tile deal (every 16-row band cut into 16-column blocks, block j
-of band b -> rank (j + 3b) % N, so expensive rows are spread over every rank; --layout
-bands keeps whole 16-row bands, band b -> rank b % N); weak tiling: 16-row bands -- each
-rank renders its share and every frame is gathered to rank 0 over RCCL as RGB8 (3 B
+fixed tiling: learned strips (round 6: rank r renders one contiguous strip of rows, the
+strips re-cut from the ranks' measured frame times before timing until their costs are
+equal -- compact like a band, balanced like the deal; --layout tiles: the 2-D tile deal,
+every 16-row band cut into 16-column blocks, block j of band b -> rank (j + 3b) % N;
+--layout bands: whole 16-row bands, band b -> rank b % N); weak tiling: 16-row bands --
+each rank renders its share and every frame is gathered to rank 0 over RCCL as RGB8 (3 B
 per pixel) and assembled there.  Tiling:
   fixed -- the config's own frame whatever N is (strong scaling; BASELINE C5 is
            defined this way: one 3840x2160 frame tiled over 8 GPUs);
@@ -90,9 +92,11 @@ def parse():
                    help="every rank on cuda:0 (rehearse N ranks on a one-GPU box; needs --backend gloo)")
     p.add_argument("--resolution", default="",
                    help="WxH instead of the config's frame (tests; the same view and scene)")
-    p.add_argument("--layout", default="auto", choices=["auto", "bands", "tiles"],
-                   help="how the frame is dealt over N > 1 ranks: 16-row bands, or the 2-D tile deal (16-row bands "
-                        "cut into --tile-cols column blocks); auto = tiles for fixed tiling, bands for weak")
+    p.add_argument("--layout", default="auto", choices=["auto", "bands", "tiles", "strips"],
+                   help="how the frame is dealt over N > 1 ranks: 16-row bands, the 2-D tile deal (16-row bands "
+                        "cut into --tile-cols column blocks), or learned strips (round 6: one contiguous strip "
+                        "of rows per rank, re-cut from the ranks' measured frame times before timing so that "
+                        "their costs are equal); auto = strips for fixed tiling, bands for weak")
     p.add_argument("--tile-cols", type=int, default=16, help="column block of the 2-D tile deal (one workgroup)")
     p.add_argument("--exchange", action="store_true",
                    help="run the N > 1 frame exchange (process group, RGB8 pack, gather, rank-0 assembly) even "
@@ -127,7 +131,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import voxelraymarcher_amd as vr  # noqa: E402
-from voxelraymarcher_amd.tiles import BandGather, frame_resolution, init_frame_group, pipeline_depth  # noqa: E402
+from voxelraymarcher_amd.tiles import (BandGather, frame_resolution, init_frame_group, pipeline_depth,  # noqa: E402
+                                       strip_bounds)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 N_SIMD = 1024              # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles (SIMD-32)
@@ -135,6 +140,46 @@ BAND_ROWS = 16             # row bands and the 2-D tile deal's bands: one 16x16 
                            # (8-row bands put two frame strips in one block: C5 rank of 8 0.099 vs
                            # 0.089 ms, C2 weak rank of 8 0.0883 vs 0.0841)
 HEADLINE = "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s"   # BASELINE.json metric
+# the learned strip deal (--layout strips): rebalancing rounds, frames timed per round (after
+# STRIP_WARM untimed ones: the learned orders of the new strip), strip boundaries on 8-row steps
+STRIP_ITERS, STRIP_WARM, STRIP_STEPS, STRIP_ALIGN = 5, 16, 80, 8
+
+
+def learn_strips(pipe, render_rows, W, H, world, rank, dev, stage_host, grouped) -> list:
+    """Re-cut pipe's strips from the ranks' frame times (tiles.rebalance_strips): each rank
+    times STRIP_STEPS frames of its own strip with pipe.depth frames in flight on pipe's own
+    streams (no exchange: a gather would make every rank wait for the slowest), the times
+    are all-reduced into one vector, and every rank re-cuts the same strips from it.  Returns
+    the rounds' (strips, times); pipe is left with the last cut."""
+    from voxelraymarcher_amd.tiles import rebalance_strips
+    bounds, est, hist = list(pipe.S), None, []
+    nst = len(pipe.streams)
+    scratch = [torch.empty(W * H, dtype=torch.int32, device=dev) for _ in range(nst)]
+    cur = torch.cuda.current_stream()
+    for _ in range(STRIP_ITERS):
+        y0, y1 = bounds[rank], bounds[rank + 1]
+
+        def loop(n):
+            for i in range(n):
+                with torch.cuda.stream(pipe.streams[i % nst]):
+                    render_rows(scratch[i % nst], y0, y1)
+
+        for st in pipe.streams:
+            st.wait_stream(cur)
+        loop(STRIP_WARM)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        loop(STRIP_STEPS)
+        torch.cuda.synchronize()
+        t = torch.zeros(world, dtype=torch.float64, device="cpu" if stage_host else dev)
+        t[rank] = (time.perf_counter() - t0) / STRIP_STEPS * 1e3
+        if grouped:
+            dist.all_reduce(t)
+        ts = [float(x) for x in t.cpu().tolist()]
+        hist.append({"strips": list(bounds), "ms_per_frame": [round(x, 4) for x in ts]})
+        bounds, est = rebalance_strips(bounds, ts, STRIP_ALIGN, prior=est)
+    pipe.set_strips(bounds)
+    return hist
 
 
 def cpu_info() -> dict:
@@ -274,14 +319,19 @@ def main():
     # N > 1: bands travel as the RGB8 framebuffer (writeColorToFramebuffer's format, 3 B per
     # pixel): rank 0 ends each frame with the RGB8 image
     depth = args.frames_in_flight or pipeline_depth(args.config)
-    layout = args.layout if args.layout != "auto" else ("tiles" if tiling == "fixed" else "bands")
+    layout = args.layout if args.layout != "auto" else ("strips" if tiling == "fixed" else "bands")
     band_rows = BAND_ROWS
+    strips0 = strip_bounds([1.0] * H, world, STRIP_ALIGN) if (layout == "strips" and grouped) else None
     pipe = BandGather(W, H, band_rows, rank, world, dev, depth=depth, rgb8=grouped, stage_host=stage_host,
-                      tile_cols=args.tile_cols if layout == "tiles" else 0, exchange=grouped)
-    tcols = pipe.T          # 0: row bands (every N = 1 run without --exchange)
+                      tile_cols=args.tile_cols if layout == "tiles" else 0, exchange=grouped, strips=strips0)
+    tcols = pipe.T          # 0: row bands or strips (every N = 1 run without --exchange)
+    strip = pipe.S is not None
 
     def render_with(c, buf):   # on the current stream (BandGather's slot stream in the loops)
-        if tcols:
+        if strip:
+            y0, y1 = pipe.rows()
+            vr.render_ex(scene, cfg.algorithm, c, lit, info, W, H, buf, y0, y1)
+        elif tcols:
             vr.render_tiles(scene, cfg.algorithm, c, lit, info, W, H, band_rows, tcols, rank, world, buf)
         else:
             vr.render_bands(scene, cfg.algorithm, c, lit, info, W, H, band_rows, rank, world, buf)
@@ -309,10 +359,21 @@ def main():
     # untimed) and of the whole frame (sum over ranks); `stats`: the part of
     # them the crawl pass credits for crawl iterations it fast-forwards in closed form
     # (their existence reads are counted, never issued)
+    # Learned strips: re-cut the strips from every rank's measured frame time of its own strip
+    # (pipelined, no exchange), STRIP_ITERS times (tiles.rebalance_strips), so that the ranks'
+    # costs are equal -- every rank computes the same cut from the same all-reduced times
+    strip_hist = []
+    if strip:
+        strip_hist = learn_strips(pipe, lambda buf, y0, y1: vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H,
+                                                                         buf, y0, y1),
+                                  W, H, world, rank, dev, stage_host, grouped)
     ctr = torch.zeros(1, dtype=torch.int64, device=dev)
     stats = torch.zeros(2, dtype=torch.int64, device=dev)
-    vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, pipe.bufs[0], band_rows=band_rows, rank=rank,
-                 nranks=world, counter=ctr, stats=stats, tile_cols=tcols)
+    if strip:
+        vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, pipe.bufs[0], *pipe.rows(), counter=ctr, stats=stats)
+    else:
+        vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, pipe.bufs[0], band_rows=band_rows, rank=rank,
+                     nranks=world, counter=ctr, stats=stats, tile_cols=tcols)
     torch.cuda.synchronize()
     launch_bytes = int(ctr.item())
     ff_iters, ff_bytes = (int(x) for x in stats.cpu().tolist())
@@ -353,6 +414,10 @@ def main():
         render(pipe.bufs[0])
 
     def render_grid(buf):
+        if strip:
+            vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, *pipe.rows(), stream=stream,
+                         schedule=vr.Schedule.GRID)
+            return
         vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=band_rows, rank=rank, nranks=world,
                      stream=stream, schedule=vr.Schedule.GRID, tile_cols=tcols)
 
@@ -516,7 +581,9 @@ def main():
              f"achieved HBM GB/s")
         gather = ("RCCL gather" if backend == "nccl" else "gloo gather staged through host memory") + \
             (" (ranks sharing cuda:0)" if args.same_device else "")
-        deal = (f"2-D tile deal x{world} ({band_rows}x{tcols} blocks, block j of {band_rows}-row band b -> rank (j + "
+        deal = (f"learned strips x{world} (rank r renders rows [b_r, b_r+1), b = {pipe.S}, cut by measured cost)"
+                if strip else
+                f"2-D tile deal x{world} ({band_rows}x{tcols} blocks, block j of {band_rows}-row band b -> rank (j + "
                 f"{pipe.stride}b) % {world})" if tcols else f"row-band tiles x{world}")
         par = deal + (f" + {gather} of the RGB8 tiles to rank 0 (overlapped with the next frame)" if grouped else "")
         line = {
@@ -546,7 +613,7 @@ def main():
                                                                        f"scaling)"),
                        "grid": cfg.grid, "width": W, "height": H, "tiling": tiling,
                        "store": cfg.store.name, "algorithm": cfg.algorithm.name, "scale": cfg.scale,
-                       "voxels": int(len(rgb)), "parallelism": par, "layout": "tiles" if tcols else "bands",
+                       "voxels": int(len(rgb)), "parallelism": par, "layout": "strips" if strip else ("tiles" if tcols else "bands"),
                        "frames_in_flight": pipe.depth,
                        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default")},
             "kernel_ms": round(kern_ms, 4),
@@ -563,10 +630,14 @@ def main():
             "roofline": roof,
             # the non-instrumented launches of this run in order, per phase (a rocprofv3 kernel
             # trace of the same command splits into them: profiles/roofline_phases.py)
-            "dispatch_phases": {"warmup": args.warmup, "iso_first": n_iso, "untimed": 40, "iso_grid": n_iso,
+            "dispatch_phases": {"strip_calibration": STRIP_ITERS * (STRIP_WARM + STRIP_STEPS) if strip else 0,
+                                "warmup": args.warmup, "iso_first": n_iso, "untimed": 40, "iso_grid": n_iso,
                                 "iso_learned": n_iso,
                                 "latency": 5 if grouped else 0, "timed": args.steps, "moving": args.steps},
         }
+        if strip:
+            line["config"]["strip_bounds"] = pipe.S
+            line["config"]["strip_calibration"] = strip_hist
         if HW_QUEUES_REQUESTED is not None:
             line["config"]["hw_queues_requested"] = HW_QUEUES_REQUESTED
         if frame_latency_ms is not None:

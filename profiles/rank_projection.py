@@ -30,8 +30,13 @@ p.add_argument("--warmup", type=int, default=20)
 p.add_argument("--frames-in-flight", type=int, default=0, help="default: tiles.pipeline_depth (bench.py's)")
 p.add_argument("--ranks", default="", help="comma-separated subset of ranks (default: all)")
 p.add_argument("--band-rows", type=int, default=16, help="bench.py's BAND_ROWS")
-p.add_argument("--layout", default="tiles", choices=["tiles", "bands"],
-               help="tiles: the 2-D deal bench.py uses for fixed tiling (round 5); bands: 8-row bands")
+p.add_argument("--layout", default="tiles", choices=["tiles", "bands", "strips"],
+               help="tiles: the 2-D deal (round 5); bands: row bands; strips: the learned cost-balanced "
+                    "contiguous strips (round 6: rank r renders rows [b_r, b_r+1), the cuts re-made from the "
+                    "ranks' measured frame times --strip-iters times, tiles.rebalance_strips)")
+p.add_argument("--strip-iters", type=int, default=5, help="strips: rebalancing rounds")
+p.add_argument("--strip-steps", type=int, default=80, help="strips: pipelined frames timed per rank per round")
+p.add_argument("--strip-align", type=int, default=8)
 p.add_argument("--tile-cols", type=int, default=16)
 p.add_argument("--latency-reps", type=int, default=30)
 p.add_argument("--tiling", default="fixed", choices=["fixed", "weak"],
@@ -63,7 +68,13 @@ lit = vr.setup_constant_values()
 info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
 B = a.band_rows
 T = a.tile_cols if a.layout == "tiles" else 0
-words = vr.tile_buffer_words(W, H, B, T, a.world) if T else vr.band_buffer_words(W, H, B, a.world)
+STRIPS = a.layout == "strips"
+bounds = None
+if STRIPS:
+    from voxelraymarcher_amd.tiles import rebalance_strips, strip_bounds  # noqa: E402
+    bounds = strip_bounds([1.0] * H, a.world, a.strip_align)     # equal heights to start
+words = (W * H if STRIPS else
+         vr.tile_buffer_words(W, H, B, T, a.world) if T else vr.band_buffer_words(W, H, B, a.world))
 
 
 # ONE pipeline (its streams) for every run: a second BandGather's new streams may share a
@@ -75,16 +86,25 @@ pipe.bufs = [torch.empty(max(words, vr.band_buffer_words(W, H, B, 1)), dtype=tor
 packed = [torch.empty(words * 3, dtype=torch.uint8, device=dev) for _ in range(depth)]
 
 
+def send_words():
+    """Words each rank sends (equal on every rank: one gather); strips pad to the tallest."""
+    if STRIPS:
+        return W * max(bounds[r + 1] - bounds[r] for r in range(a.world))
+    return words
+
+
 def run(rank, nranks, steps):
     k = [0]
 
     def render(buf):
-        if T and nranks > 1:
+        if STRIPS and nranks > 1:
+            vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, bounds[rank], bounds[rank + 1])
+        elif T and nranks > 1:
             vr.render_tiles(scene, cfg.algorithm, cam, lit, info, W, H, B, T, rank, nranks, buf)
         else:
             vr.render_bands(scene, cfg.algorithm, cam, lit, info, W, H, B, rank, nranks, buf)
         if nranks > 1:                                  # the send side of bench.py's N > 1 step
-            vr.pack_rgb8(buf[:words], out=packed[k[0] % depth])
+            vr.pack_rgb8(buf[:send_words()], out=packed[k[0] % depth][:3 * send_words()])
         k[0] += 1
 
     for _ in range(a.warmup):
@@ -105,10 +125,14 @@ def lone(rank, nranks, schedule):
     buf = pipe.bufs[0]
 
     def once():
-        vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=B, rank=rank, nranks=nranks,
-                     stream=st, schedule=schedule, tile_cols=T if nranks > 1 else 0)
+        if STRIPS and nranks > 1:
+            vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, bounds[rank], bounds[rank + 1],
+                         stream=st, schedule=schedule)
+        else:
+            vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=B, rank=rank, nranks=nranks,
+                         stream=st, schedule=schedule, tile_cols=T if nranks > 1 else 0)
         if nranks > 1:
-            vr.pack_rgb8(buf[:words], out=packed[0])
+            vr.pack_rgb8(buf[:send_words()], out=packed[0][:3 * send_words()])
 
     for _ in range(20):
         once()
@@ -126,6 +150,15 @@ def lone(rank, nranks, schedule):
 
 single = run(0, 1, a.steps)
 single_lone = {k: lone(0, 1, s) for k, s in (("grid", vr.Schedule.GRID), ("learned", vr.Schedule.HEAVIEST_FIRST))}
+calibration = []
+if STRIPS:
+    # the learned strip deal: each round times every rank's strip pipelined and re-cuts
+    est = None
+    for it in range(a.strip_iters):
+        ts = [run(r, a.world, a.strip_steps) for r in range(a.world)]
+        calibration.append({"bounds": list(bounds), "ms_per_frame": [round(t, 4) for t in ts]})
+        print(json.dumps({"strip_round": it, **calibration[-1]}), flush=True)
+        bounds, est = rebalance_strips(bounds, ts, a.strip_align, prior=est)
 ranks = []
 for r in ([int(x) for x in a.ranks.split(",")] if a.ranks else range(a.world)):
     ms = run(r, a.world, a.steps)
@@ -140,7 +173,7 @@ slow_ll = max(x["lone_frame_ms_learned"] for x in ranks)
 mean = sum(x["ms_per_frame"] for x in ranks) / len(ranks)
 mean_lg = sum(x["lone_frame_ms_grid"] for x in ranks) / len(ranks)
 print(json.dumps({"config": a.config, "width": W, "height": H, "world": a.world, "band_rows": B,
-                  "layout": a.layout, "tile_cols": T,
+                  "layout": a.layout, "tile_cols": T, "strip_bounds": bounds, "strip_calibration": calibration,
                   "slowest_over_mean": round(slow / mean, 3), "slowest_over_mean_lone_grid": round(slow_lg / mean_lg, 3),
                   "frames_in_flight": depth,
                   "steps": a.steps, "one_gpu_ms_per_frame": round(single, 4),

@@ -275,3 +275,61 @@ def test_forced_exchange_single_rank():
     ok = q.get(timeout=120)
     p.join(timeout=60)
     assert p.exitcode == 0 and ok
+
+
+def _strip_pipeline_worker(rank, world, port, W, H, frames, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from voxelraymarcher_amd.tiles import BandGather, rebalance_strips, strip_bounds
+
+    def expected(k):
+        return ((torch.arange(W * H, dtype=torch.int64) * 2654435761 + 977 * k) % (1 << 24)).to(torch.int32).reshape(H, W)
+
+    # the learned strip deal as bench.py makes it: equal strips, then re-cut from every rank's
+    # (here: made-up, rank-dependent) frame times, the same on every rank (all_reduce of the vector)
+    bounds = strip_bounds([1.0] * H, world, 8)
+    got = []
+    pipe = BandGather(W, H, 8, rank, world, "cpu", depth=2, on_frame=lambda f: got.append(f.clone()), strips=bounds)
+    k_box = [0]
+
+    def render(buf):
+        y0, y1 = pipe.rows()
+        buf[:(y1 - y0) * W].copy_(expected(k_box[0])[y0:y1].reshape(-1))
+
+    for k in range(frames):                      # frames on the equal strips
+        k_box[0] = k
+        pipe.step(render)
+    pipe.drain()
+    t = torch.zeros(world, dtype=torch.float64)
+    t[rank] = (bounds[rank + 1] - bounds[rank]) * (1.0 + rank)
+    dist.all_reduce(t)
+    new, _ = rebalance_strips(bounds, t.tolist(), 8)
+    pipe.set_strips(new)
+    for k in range(frames, 2 * frames):          # frames on the re-cut strips
+        k_box[0] = k
+        pipe.step(render)
+    pipe.drain()
+    if rank == 0:
+        q.put(([bool(torch.equal(g, expected(k))) for k, g in enumerate(got)], bounds, new))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_strip_gather_pipeline_overlapped(world):
+    """BandGather with the learned strip deal (round 6): frames intact and in order, two in
+    flight, before and after the strips are re-cut from the ranks' times (set_strips); the
+    re-cut gives the slower (higher-rank) strips fewer rows."""
+    W, H, frames = 40, 77, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_strip_pipeline_worker, args=(r, world, port, W, H, frames, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res, b0, b1 = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [True] * (2 * frames)
+    assert b1 != b0 and (b1[world] - b1[world - 1]) < (b0[world] - b0[world - 1])

@@ -59,24 +59,26 @@ def _run_bench(world, extra, tmp_path, W=480, H=270):
     return json.loads(lines[0]), np.load(dump)
 
 
-def test_rccl_gather_one_rank(tmp_path):
+@pytest.mark.parametrize("layout", ["tiles", "strips"])
+def test_rccl_gather_one_rank(tmp_path, layout):
     """The RCCL branch of the N > 1 path on a one-GPU box (RCCL refuses two ranks on one
     device): bench.py --exchange --backend nccl starts a one-rank nccl process group
     (init_process_group("nccl", device_id=...), tiles.init_frame_group), renders the 2-D tile
-    layout, packs RGB8, gathers it with dist.gather on the slot stream over RCCL, and rank 0
-    assembles it with the device kernel (vr_assemble_tiles) on its side stream; the frame
-    equals the oracle's, byte for byte."""
+    layout (or the learned strips, fixed tiling's default since round 6: calibrated, then one
+    strip), packs RGB8, gathers it with dist.gather on the slot stream over RCCL, and rank 0
+    assembles it (vr_assemble_tiles / the strip copies) on its side stream; the frame equals
+    the oracle's, byte for byte."""
     W, H = 480, 270
-    line, got = _run_bench(1, ["--exchange", "--backend", "nccl"], tmp_path, W, H)
+    line, got = _run_bench(1, ["--exchange", "--backend", "nccl", "--layout", layout], tmp_path, W, H)
     assert line["n_gpus"] == 1 and "RCCL gather" in line["config"]["parallelism"]
-    assert line["config"]["layout"] == "tiles" and line["dispatch_phases"]["latency"] == 5
+    assert line["config"]["layout"] == layout and line["dispatch_phases"]["latency"] == 5
     want = _oracle_rgb8("C2", W, H)
     assert got.shape == (H, W, 3) and got.dtype == np.uint8
     bad = int(np.count_nonzero(np.any(got != want, axis=-1)))
     assert bad == 0, f"{bad} of {W * H} pixels of the RCCL-gathered RGB8 frame differ from the oracle"
 
 
-@pytest.mark.parametrize("world,layout", [(2, "tiles"), (3, "tiles"), (2, "bands")])
+@pytest.mark.parametrize("world,layout", [(2, "tiles"), (3, "tiles"), (2, "bands"), (2, "strips"), (3, "strips")])
 def test_bench_frame_path_ranks_share_one_gpu(world, layout, tmp_path):
     W, H = 480, 270
     dump = tmp_path / "frame.npy"
@@ -96,6 +98,10 @@ def test_bench_frame_path_ranks_share_one_gpu(world, layout, tmp_path):
     assert line["frame_latency_ms"] > 0 and line["ms_per_step"] > 0 and line["value"] > 0
     assert "gloo" in line["config"]["parallelism"] and line["config"]["layout"] == layout
     assert line["dispatch_phases"]["latency"] == 5
+    if layout == "strips":                   # learned: calibrated, re-cut, every row dealt once
+        b = line["config"]["strip_bounds"]
+        assert len(b) == world + 1 and b[0] == 0 and b[-1] == H and all(b[i] < b[i + 1] for i in range(world))
+        assert len(line["config"]["strip_calibration"]) >= 1
     # the frame's algorithmic bytes are the sum over the ranks' bands (all-reduced)
     assert line["roofline"]["algorithmic_bytes_per_frame"] > line["roofline"]["algorithmic_bytes_per_launch"]
     got = np.load(dump)

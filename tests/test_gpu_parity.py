@@ -169,13 +169,15 @@ def test_c5_crawl_pixels_fixture(c5):
                 assert int(got[(p["y"] - 696) * cfg.width + p["x"]]) == p["colour"], p
 
 
-@pytest.mark.parametrize("layout", ["tiles", "bands"])
+@pytest.mark.parametrize("layout", ["tiles", "bands", "strips"])
 def test_c5_eight_rank_emulation(c5, layout):
     """C5 as BASELINE defines it -- the fixed 3840x2160 frame over 8 ranks -- emulated on
     one GPU: each rank's buffer, assembled, equals the oracle's frame.  layout "tiles":
     the 2-D deal bench.py uses (16x16 blocks, block j of band b -> rank (j + 3b) % 8;
     vr_render_tiles + the device assembly kernel), both algorithms; "bands": 8-row bands
-    dealt round-robin (vr_render_bands)."""
+    dealt round-robin (vr_render_bands); "strips": the learned strip deal (round 6, the fixed
+    tiling default) with the cut the calibration made on an MI355X (profiles/r06/strips/): rank
+    r renders rows [b_r, b_r+1) (vr_render_ex), both algorithms, assembled by the host copies."""
     import torch
 
     from voxelraymarcher_amd.tiles import assemble_bands
@@ -184,8 +186,17 @@ def test_c5_eight_rank_emulation(c5, layout):
     B = 16 if layout == "tiles" else 8
     cam, lit = vr.Camera.reference(W, H), vr.setup_constant_values()
     info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
-    for algo in (ALGOS if layout == "tiles" else [vr.RayMarchAlgorithm.ORIGINAL]):
-        if layout == "tiles":
+    for algo in (ALGOS if layout != "bands" else [vr.RayMarchAlgorithm.ORIGINAL]):
+        if layout == "strips":
+            from voxelraymarcher_amd.tiles import assemble_strips
+            b = [0, 216, 464, 688, 840, 1056, 1296, 1632, 2160]
+            mh = max(b[r + 1] - b[r] for r in range(R))
+            parts = torch.full((R, mh * W), -7, dtype=torch.int32, device="cuda")
+            for r in range(R):
+                vr.render_ex(g, algo, cam, lit, info, W, H, parts[r], b[r], b[r + 1])
+            torch.cuda.synchronize()
+            img = assemble_strips(parts, b, W).cpu().numpy().view(np.uint32).reshape(-1)
+        elif layout == "tiles":
             words = vr.tile_buffer_words(W, H, B, T, R)
             parts = torch.full((R, words), -7, dtype=torch.int32, device="cuda")
             for r in range(R):

@@ -75,3 +75,54 @@ def test_tile_entry_points_validate_arguments():
     assert b"elem_bytes" in lib.vr_last_error()
     assert lib.vr_assemble_tiles(buf, buf, 4, 64, 64, 8, 128, 2, 0, None) == -1
     assert lib.vr_tile_buffer_words(64, 64, 8, 0, 2) == 0
+
+
+def test_strip_bounds_balance_and_alignment():
+    """The cost-balanced contiguous deal (tiles.strip_bounds): strips are contiguous, cover
+    every row once, start on aligned rows, and their costs are as equal as the alignment
+    allows -- an expensive band of rows (C5's crawl rows) gets a short strip."""
+    from voxelraymarcher_amd.tiles import strip_bounds
+    H = 2160
+    cost = [1.0] * H
+    for y in range(680, 720):
+        cost[y] = 10.0
+    b = strip_bounds(cost, 8, 8)
+    assert b[0] == 0 and b[-1] == H and all(b[i] < b[i + 1] for i in range(8))
+    assert all(x % 8 == 0 for x in b[:-1])
+    per = [sum(cost[b[r]:b[r + 1]]) for r in range(8)]
+    assert max(per) / (sum(per) / 8) < 1.05, per
+    assert min(b[r + 1] - b[r] for r in range(8)) < 200 < max(b[r + 1] - b[r] for r in range(8))
+    # uniform costs: equal heights (to the alignment)
+    u = strip_bounds([1.0] * 1080, 4, 8)
+    assert [u[r + 1] - u[r] for r in range(4)] == [272, 264, 272, 272] or max(
+        u[r + 1] - u[r] for r in range(4)) - min(u[r + 1] - u[r] for r in range(4)) <= 8
+
+
+def test_rebalance_strips_converges():
+    """tiles.rebalance_strips: timing each strip and re-cutting moves rows from the slow ranks to
+    the fast ones; on a fixed hidden cost it reaches max/mean < 1.05 in a few rounds."""
+    from voxelraymarcher_amd.tiles import rebalance_strips, strip_bounds
+    H, N = 2160, 8
+    true = [0.2 + (3.0 if 600 <= y < 760 else 0.0) + (0.0 if y > 1700 else 1.0) for y in range(H)]
+    b = strip_bounds([1.0] * H, N, 8)
+    est = None
+    for _ in range(6):
+        t = [sum(true[b[r]:b[r + 1]]) for r in range(N)]
+        b, est = rebalance_strips(b, t, 8, prior=est)
+    t = [sum(true[b[r]:b[r + 1]]) for r in range(N)]
+    assert max(t) / (sum(t) / N) < 1.05, t
+
+
+def test_assemble_strips_roundtrip():
+    import torch
+
+    from voxelraymarcher_amd.tiles import assemble_strips
+    W, H = 37, 53
+    frame = torch.arange(W * H * 3, dtype=torch.int64).reshape(H, W * 3)
+    b = [0, 8, 24, 53]
+    mh = max(b[i + 1] - b[i] for i in range(3))
+    parts = torch.full((3, mh * W * 3), -1, dtype=torch.int64)
+    for r in range(3):
+        h = b[r + 1] - b[r]
+        parts[r, :h * W * 3] = frame[b[r]:b[r + 1]].reshape(-1)
+    assert torch.equal(assemble_strips(parts, b, W, 3), frame)

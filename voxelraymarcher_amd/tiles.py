@@ -91,6 +91,75 @@ def tile_rank_buffer(frame: torch.Tensor, rank: int, nranks: int, band_rows: int
     return buf
 
 
+def strip_bounds(row_cost, nranks: int, align: int = 8) -> list[int]:
+    """The cost-balanced contiguous deal (round 6): cut rows [0, H) into nranks strips of
+    about equal cost -- rank r renders rows [b[r], b[r+1]) -- from a cost per row (any
+    non-negative weights, len = H).  Every boundary but H is a multiple of `align` rows and
+    every strip holds at least one aligned block.  A strip is the most compact share of the
+    frame a rank can have (its waves walk neighbouring rays: a rank of 8 issues its pixels
+    ~13 % more efficiently than with the 2-D tile deal, profiles/r06/deal/), and equal costs
+    keep the ranks balanced, which equal-height strips are not (C5: 0.040-0.117 ms)."""
+    H = len(row_cost)
+    nblk = -(-H // align)
+    if nranks < 1 or nblk < nranks:
+        raise ValueError(f"{H} rows in blocks of {align} cannot be cut into {nranks} strips")
+    blk = [float(sum(row_cost[i * align:(i + 1) * align])) for i in range(nblk)]
+    cum = [0.0]
+    for c in blk:
+        cum.append(cum[-1] + max(c, 0.0))
+    # the contiguous partition that minimises the costliest strip (exact dynamic programme over
+    # block edges: best[k][e] = the least possible max cost of k strips covering blocks [0, e))
+    inf = float("inf")
+    best = [[inf] * (nblk + 1) for _ in range(nranks + 1)]
+    arg = [[0] * (nblk + 1) for _ in range(nranks + 1)]
+    best[0][0] = 0.0
+    for k in range(1, nranks + 1):
+        prev, cur, ak = best[k - 1], best[k], arg[k]
+        for e in range(k, nblk - (nranks - k) + 1):
+            m, mj = inf, k - 1
+            for j in range(e - 1, k - 2, -1):       # the last strip is blocks [j, e)
+                last = cum[e] - cum[j]
+                if last >= m:
+                    break                           # (only grows as j falls)
+                v = prev[j] if prev[j] > last else last
+                if v < m:
+                    m, mj = v, j
+            cur[e], ak[e] = m, mj
+    cuts, e = [nblk], nblk
+    for k in range(nranks, 0, -1):
+        e = arg[k][e]
+        cuts.append(e)
+    cuts.reverse()
+    return [c * align for c in cuts[:-1]] + [H]
+
+
+def rebalance_strips(bounds, times, align: int = 8, prior=None, damping: float = 0.5):
+    """One step of the learned strip deal: from the strips `bounds` and each rank's measured
+    time for its strip, a cost per row (time / height, uniform within each strip), averaged
+    with the previous estimate `prior` (a per-row cost list, weight `damping` on the new
+    one) and re-cut by strip_bounds.  Returns (new bounds, the per-row cost estimate)."""
+    H = bounds[-1]
+    est = [0.0] * H
+    for r in range(len(bounds) - 1):
+        h = bounds[r + 1] - bounds[r]
+        for y in range(bounds[r], bounds[r + 1]):
+            est[y] = float(times[r]) / h
+    if prior is not None:
+        est = [damping * e + (1.0 - damping) * p for e, p in zip(est, prior)]
+    return strip_bounds(est, len(bounds) - 1, align), est
+
+
+def assemble_strips(parts: torch.Tensor, bounds, width: int, px: int = 1) -> torch.Tensor:
+    """parts: [R, >= max_h * width * px] per-rank strip buffers (rank r's rows [b[r], b[r+1])
+    first, padding after) -> [H, width * px] frame.  (Rank 0 on a GPU does the same copies.)"""
+    H = bounds[-1]
+    out = torch.empty((H, width * px), dtype=parts.dtype, device=parts.device)
+    for r in range(len(bounds) - 1):
+        h = bounds[r + 1] - bounds[r]
+        out[bounds[r]:bounds[r + 1]] = parts[r, :h * width * px].view(h, width * px)
+    return out
+
+
 def owned_rows(height: int, band_rows: int, rank: int, nranks: int) -> list[int]:
     """Frame rows rendered by `rank` (for tests and accounting)."""
     rows = []
@@ -185,42 +254,42 @@ class BandGather:
 
     def __init__(self, width: int, height: int, band_rows: int, rank: int, nranks: int,
                  device, depth: int = 2, on_frame=None, rgb8: bool = False, stage_host: bool = False,
-                 tile_cols: int = 0, stride: int = 0, exchange: bool | None = None):
+                 tile_cols: int = 0, stride: int = 0, exchange: bool | None = None, strips=None):
         self.W, self.H, self.B = width, height, band_rows
         self.rank, self.R, self.depth = rank, nranks, depth
         # exchange: gather every frame to rank 0 and assemble it there (N > 1; with one rank it
         # is forced only to run that code -- RCCL included -- on a one-GPU box)
         self.x = nranks > 1 if exchange is None else bool(exchange)
         x = self.x
+        # strips (round 6, the learned cost-balanced contiguous deal): rank r renders rows
+        # [strips[r], strips[r+1]) into the first rows of its buffer; every buffer holds the
+        # tallest strip (one gather of equal buffers) and rank 0 copies each strip into place
+        self.S = list(strips) if (strips is not None and x) else None
+        if self.S is not None and (len(self.S) != nranks + 1 or self.S[0] != 0 or self.S[-1] != height or
+                                   any(self.S[i] >= self.S[i + 1] for i in range(nranks))):
+            raise ValueError(f"strips {strips} do not cut rows [0, {height}) into {nranks} strips")
         # the 2-D tile deal (with the exchange only: without it the band buffer is the frame)
-        self.T = int(tile_cols) if x else 0
+        self.T = int(tile_cols) if (x and self.S is None) else 0
         self.stride = deal_stride(nranks, stride) if self.T else 0
-        words = (tile_words(width, height, band_rows, self.T, nranks) if self.T else
+        words = (width * max(self.S[i + 1] - self.S[i] for i in range(nranks)) if self.S is not None else
+                 tile_words(width, height, band_rows, self.T, nranks) if self.T else
                  band_buffer_words(width, height, band_rows, nranks))
-        self.words = words
-        self.per = bands_per_rank(height, band_rows, nranks)
-        self.bufs = [torch.empty(words, dtype=torch.int32, device=device) for _ in range(depth)]
-        # rgb8 (GPUs, N > 1): the bands travel as the RGB8 framebuffer (3 B per pixel
-        # instead of the 4-B packed word: a quarter less over xGMI) and rank 0
-        # assembles an RGB8 frame [H, W, 3]
-        self.rgb8 = bool(rgb8) and x
-        self.px = 3 if self.rgb8 else 1                  # elements per pixel in the exchanged buffers
-        xdt = torch.uint8 if self.rgb8 else torch.int32
-        self.packed = ([torch.empty(words * 3, dtype=torch.uint8, device=device) for _ in range(depth)]
-                       if self.rgb8 else None)
-        self.recv = ([torch.empty((nranks, words * self.px), dtype=xdt, device=device) for _ in range(depth)]
-                     if (rank == 0 and x) else None)
+        self.device = device
+        self.xdt = torch.uint8 if (bool(rgb8) and x) else torch.int32
         # stage_host (a gloo group over GPU buffers -- gloo gathers host tensors only, e.g.
         # several ranks sharing one GPU, where RCCL refuses): each frame's send buffer is
         # copied to pinned host memory once its render is complete, gathered there, and the
         # receive buffers are copied back to the device before the same assembly
         self.stage = bool(stage_host) and x and torch.device(device).type == "cuda"
-        if self.stage:
-            self.h_send = [torch.empty(words * self.px, dtype=xdt, pin_memory=True) for _ in range(depth)]
-            self.h_recv = ([torch.empty((nranks, words * self.px), dtype=xdt, pin_memory=True) for _ in range(depth)]
-                           if rank == 0 else None)
-        frame_rows = height if self.T else self.per * nranks * band_rows
-        self.frame = (torch.empty((frame_rows, width * self.px), dtype=xdt, device=device)
+        # rgb8 (GPUs, N > 1): the bands travel as the RGB8 framebuffer (3 B per pixel
+        # instead of the 4-B packed word: a quarter less over xGMI) and rank 0
+        # assembles an RGB8 frame [H, W, 3]
+        self.rgb8 = bool(rgb8) and x
+        self.px = 3 if self.rgb8 else 1                  # elements per pixel in the exchanged buffers
+        self.per = bands_per_rank(height, band_rows, nranks)
+        self._alloc(words)
+        frame_rows = height if (self.T or self.S is not None) else self.per * nranks * band_rows
+        self.frame = (torch.empty((frame_rows, width * self.px), dtype=self.xdt, device=device)
                       if rank == 0 else None)
         self.work = [None] * depth
         dev = torch.device(device)
@@ -236,12 +305,51 @@ class BandGather:
         self.k = 0
         self.last = 0                # the slot of the latest step
 
+    def _alloc(self, words: int) -> None:
+        """The per-slot buffers of `words` pixels per rank (band buffers, RGB8 send buffers, rank
+        0's receive buffers, pinned staging buffers)."""
+        depth, nranks, device, xdt = self.depth, self.R, self.device, self.xdt
+        self.words = words
+        self.bufs = [torch.empty(words, dtype=torch.int32, device=device) for _ in range(depth)]
+        self.packed = ([torch.empty(words * 3, dtype=torch.uint8, device=device) for _ in range(depth)]
+                       if self.rgb8 else None)
+        self.recv = ([torch.empty((nranks, words * self.px), dtype=xdt, device=device) for _ in range(depth)]
+                     if (self.rank == 0 and self.x) else None)
+        if self.stage:
+            self.h_send = [torch.empty(words * self.px, dtype=xdt, pin_memory=True) for _ in range(depth)]
+            self.h_recv = ([torch.empty((nranks, words * self.px), dtype=xdt, pin_memory=True) for _ in range(depth)]
+                           if self.rank == 0 else None)
+
+    def set_strips(self, strips) -> None:
+        """Re-cut the strip deal (learned strips: bench.py re-cuts them from the ranks' measured
+        frame times before timing); only between drained frames.  Buffers are re-made for the
+        new tallest strip; the streams are kept."""
+        if self.S is None:
+            raise ValueError("not a strip deal")
+        if self.pending:
+            raise RuntimeError("set_strips with frames in flight: drain() first")
+        S = list(strips)
+        if len(S) != self.R + 1 or S[0] != 0 or S[-1] != self.H or any(S[i] >= S[i + 1] for i in range(self.R)):
+            raise ValueError(f"strips {strips} do not cut rows [0, {self.H}) into {self.R} strips")
+        if self.streams is not None:
+            torch.cuda.synchronize(self.device)        # (the old buffers' last users are done)
+        self.S = S
+        self._alloc(self.W * max(S[i + 1] - S[i] for i in range(self.R)))
+
+    def rows(self) -> tuple[int, int]:
+        """This rank's strip (strip deal only)."""
+        return self.S[self.rank], self.S[self.rank + 1]
+
     def _slot_stream(self, slot: int):
         return torch.cuda.stream(self.streams[slot]) if self.streams is not None else contextlib.nullcontext()
 
     def _assemble(self, slot: int) -> None:
         rw = self.W * self.px
-        if self.T:
+        if self.S is not None:                             # one copy per strip
+            for r in range(self.R):
+                y0, y1 = self.S[r], self.S[r + 1]
+                self.frame[y0:y1].copy_(self.recv[slot][r, :(y1 - y0) * rw].view(y1 - y0, rw))
+        elif self.T:
             if self.recv[slot].is_cuda:                    # one un-dealing kernel (vr_assemble_tiles)
                 from .renderer import assemble_tiles_device
                 eb = self.px * self.recv[slot].element_size()
