@@ -34,7 +34,7 @@ p.add_argument("--layout", default="tiles", choices=["tiles", "bands", "strips"]
                help="tiles: the 2-D deal (round 5); bands: row bands; strips: the learned cost-balanced "
                     "contiguous strips (round 6: rank r renders rows [b_r, b_r+1), the cuts re-made from the "
                     "ranks' measured frame times --strip-iters times, tiles.rebalance_strips)")
-p.add_argument("--strip-iters", type=int, default=5, help="strips: rebalancing rounds")
+p.add_argument("--strip-iters", type=int, default=8, help="strips: rebalancing rounds")
 p.add_argument("--strip-steps", type=int, default=80, help="strips: pipelined frames timed per rank per round")
 p.add_argument("--strip-align", type=int, default=8)
 p.add_argument("--tile-cols", type=int, default=16)
@@ -159,6 +159,8 @@ if STRIPS:
         calibration.append({"bounds": list(bounds), "ms_per_frame": [round(t, 4) for t in ts]})
         print(json.dumps({"strip_round": it, **calibration[-1]}), flush=True)
         bounds, est = rebalance_strips(bounds, ts, a.strip_align, prior=est)
+    # as bench.py: the measured cut whose slowest rank was fastest
+    bounds = min(calibration, key=lambda c: max(c["ms_per_frame"]))["bounds"]
 ranks = []
 for r in ([int(x) for x in a.ranks.split(",")] if a.ranks else range(a.world)):
     ms = run(r, a.world, a.steps)
