@@ -141,8 +141,10 @@ BAND_ROWS = 16             # row bands and the 2-D tile deal's bands: one 16x16 
                            # 0.089 ms, C2 weak rank of 8 0.0883 vs 0.0841)
 HEADLINE = "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s"   # BASELINE.json metric
 # the learned strip deal (--layout strips): rebalancing rounds, frames timed per round (after
-# STRIP_WARM untimed ones: the learned orders of the new strip), strip boundaries on 8-row steps
-STRIP_ITERS, STRIP_WARM, STRIP_STEPS, STRIP_ALIGN = 8, 16, 80, 8
+# STRIP_WARM untimed ones: the learned orders of the new strip), strip boundaries on 4-row steps
+# (C5 8-rank projection 6.48x with 12 rounds on 4-row steps, 6.40x with 8 on 8-row steps;
+# profiles/r06/strips/)
+STRIP_ITERS, STRIP_WARM, STRIP_STEPS, STRIP_ALIGN = 12, 16, 80, 4
 
 
 def learn_strips(pipe, render_rows, W, H, world, rank, dev, stage_host, grouped) -> list:

@@ -34,9 +34,9 @@ p.add_argument("--layout", default="tiles", choices=["tiles", "bands", "strips"]
                help="tiles: the 2-D deal (round 5); bands: row bands; strips: the learned cost-balanced "
                     "contiguous strips (round 6: rank r renders rows [b_r, b_r+1), the cuts re-made from the "
                     "ranks' measured frame times --strip-iters times, tiles.rebalance_strips)")
-p.add_argument("--strip-iters", type=int, default=8, help="strips: rebalancing rounds")
+p.add_argument("--strip-iters", type=int, default=12, help="strips: rebalancing rounds")
 p.add_argument("--strip-steps", type=int, default=80, help="strips: pipelined frames timed per rank per round")
-p.add_argument("--strip-align", type=int, default=8)
+p.add_argument("--strip-align", type=int, default=4)
 p.add_argument("--tile-cols", type=int, default=16)
 p.add_argument("--latency-reps", type=int, default=30)
 p.add_argument("--tiling", default="fixed", choices=["fixed", "weak"],
