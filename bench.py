@@ -332,17 +332,14 @@ def main():
     tcols = pipe.T          # 0: row bands or strips (every N = 1 run without --exchange)
     strip = pipe.S is not None
 
-    def render_with(c, buf):   # on the current stream (BandGather's slot stream in the loops)
+    def prepare(c):
+        """The launch of view `c` with its arguments made once (renderer.PreparedRender: the
+        timed loop's host path per frame is one ctypes call on the slot's stream)."""
         if strip:
             y0, y1 = pipe.rows()
-            vr.render_ex(scene, cfg.algorithm, c, lit, info, W, H, buf, y0, y1)
-        elif tcols:
-            vr.render_tiles(scene, cfg.algorithm, c, lit, info, W, H, band_rows, tcols, rank, world, buf)
-        else:
-            vr.render_bands(scene, cfg.algorithm, c, lit, info, W, H, band_rows, rank, world, buf)
-
-    def render(buf):
-        render_with(cam, buf)
+            return vr.PreparedRender(scene, cfg.algorithm, c, lit, info, W, H, row_begin=y0, row_end=y1)
+        return vr.PreparedRender(scene, cfg.algorithm, c, lit, info, W, H, band_rows=band_rows, rank=rank,
+                                 nranks=world, tile_cols=tcols)
 
     # A moving view (ADVICE r5): the same camera with its eye moved by 1, 2 and 3 ulps in x,
     # one per frame in turn, so no two consecutive launches -- and no launch slot's successive
@@ -356,10 +353,6 @@ def main():
         moving.append(c)
     moving_step = [0]
 
-    def render_moving(buf):
-        render_with(moving[moving_step[0] % 3], buf)
-        moving_step[0] += 1
-
     # algorithmic bytes of THIS rank's launch (its bands; instrumented kernel,
     # untimed) and of the whole frame (sum over ranks); `stats`: the part of
     # them the crawl pass credits for crawl iterations it fast-forwards in closed form
@@ -372,6 +365,14 @@ def main():
         strip_hist = learn_strips(pipe, lambda buf, y0, y1: vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H,
                                                                          buf, y0, y1),
                                   W, H, world, rank, dev, stage_host, grouped)
+    render = prepare(cam)                       # (after the strips are learned: their rows are final)
+    moving_prep = [prepare(c) for c in moving]
+
+    def render_moving(buf, stream=None):
+        moving_prep[moving_step[0] % 3](buf, stream)
+        moving_step[0] += 1
+    render_moving.vr_stream_arg = True
+
     ctr = torch.zeros(1, dtype=torch.int64, device=dev)
     stats = torch.zeros(2, dtype=torch.int64, device=dev)
     if strip:
@@ -391,54 +392,61 @@ def main():
     pipe.drain()
     torch.cuda.synchronize()
 
-    # kernel-only timing of this rank's launch on the launch stream (HIP events; the
-    # events bracket the whole launch: tile pass + crawl pass), at least 200 launches:
-    # enough samples for kernel_ms, and the GPU reaches its loaded clock before the
-    # timed loop starts (a short --steps run otherwise measures the clock ramp of a
-    # GPU that sat idle while the host built the scene)
-    # Launches on ONE stream run one after the other, so vr_render's AUTO schedule dispatches
-    # their heaviest tile groups first (from costs an earlier launch of the slot recorded:
-    # the untimed launches below make them); the pipelined loop's launches overlap on
-    # BandGather's streams and run in grid order (include/vr.h vr_schedule).  The same
-    # launches in grid order are timed too (kernel_ms_grid_order).
-    # One event pair brackets each phase of n_iso launches (an event pair around every
-    # launch adds ~10 us of event processing to each, profiles/r04/run1: 160.6 vs 150.8 us):
-    # kernel_ms = phase time / n_iso -- each launch's tile and crawl passes plus the
-    # dispatch gaps between back-to-back launches on one stream.
-    n_iso = max(args.steps, 200)
-    # A first render of the view, n_iso times: what the device learned (work and lane orders,
-    # include/vr.h vr_forget_orders) is dropped before every launch, so each one renders as
-    # the reference's one-frame CLI run does (Main.cu:105-163) -- grid order, 8x8 tiles
-    ev_first = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    ev_first[0].record(stream)
-    for _ in range(n_iso):
-        vr.forget_orders(dev.index)
-        render(pipe.bufs[0])
-    ev_first[1].record(stream)
-    for _ in range(40):
-        render(pipe.bufs[0])
-
-    def render_grid(buf):
-        if strip:
-            vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, *pipe.rows(), stream=stream,
-                         schedule=vr.Schedule.GRID)
-            return
-        vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=band_rows, rank=rank, nranks=world,
-                     stream=stream, schedule=vr.Schedule.GRID, tile_cols=tcols)
-
-    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    ev_grid = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    for (a, b), fn in ((ev_grid, render_grid), (ev, render)):
-        a.record(stream)
+    def iso_phase():
+        # kernel-only timing of this rank's launch on the launch stream (HIP events; the
+        # events bracket the whole launch: tile pass + crawl pass), at least 200 launches:
+        # enough samples for kernel_ms, and the GPU reaches its loaded clock before the
+        # timed loop starts (a short --steps run otherwise measures the clock ramp of a
+        # GPU that sat idle while the host built the scene)
+        # Launches on ONE stream run one after the other, so vr_render's AUTO schedule dispatches
+        # their heaviest tile groups first (from costs an earlier launch of the slot recorded:
+        # the untimed launches below make them); the pipelined loop's launches overlap on
+        # BandGather's streams and run in grid order (include/vr.h vr_schedule).  The same
+        # launches in grid order are timed too (kernel_ms_grid_order).
+        # One event pair brackets each phase of n_iso launches (an event pair around every
+        # launch adds ~10 us of event processing to each, profiles/r04/run1: 160.6 vs 150.8 us):
+        # kernel_ms = phase time / n_iso -- each launch's tile and crawl passes plus the
+        # dispatch gaps between back-to-back launches on one stream.
+        n_iso = max(args.steps, 200)
+        # A first render of the view, n_iso times: what the device learned (work and lane orders,
+        # include/vr.h vr_forget_orders) is dropped before every launch, so each one renders as
+        # the reference's one-frame CLI run does (Main.cu:105-163) -- grid order, 8x8 tiles
+        ev_first = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev_first[0].record(stream)
         for _ in range(n_iso):
-            fn(pipe.bufs[0])
-        b.record(stream)
-    torch.cuda.synchronize()
-    # (the events are read after the timed loop: reading 200 of them takes ~17 ms,
-    # long enough for an idle GPU to drop its clock before the timed loop starts)
-    # (the W warmup steps stay BEFORE this phase: moved to just before the timed loop
-    # they made a 20-step loop slower, 0.1196-0.1205 -> 0.128 ms per step on one box,
-    # profiles/r03/driver_ab/)
+            vr.forget_orders(dev.index)
+            render(pipe.bufs[0])
+        ev_first[1].record(stream)
+        for _ in range(40):
+            render(pipe.bufs[0])
+
+        def render_grid(buf):
+            if strip:
+                vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, *pipe.rows(), stream=stream,
+                             schedule=vr.Schedule.GRID)
+                return
+            vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, buf, band_rows=band_rows, rank=rank, nranks=world,
+                         stream=stream, schedule=vr.Schedule.GRID, tile_cols=tcols)
+
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev_grid = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        for (a, b), fn in ((ev_grid, render_grid), (ev, render)):
+            a.record(stream)
+            for _ in range(n_iso):
+                fn(pipe.bufs[0])
+            b.record(stream)
+        torch.cuda.synchronize()
+        # (the events are read after the timed loop: reading 200 of them takes ~17 ms,
+        # long enough for an idle GPU to drop its clock before the timed loop starts)
+        # (the W warmup steps stay BEFORE this phase: moved to just before the timed loop
+        # they made a 20-step loop slower, 0.1196-0.1205 -> 0.128 ms per step on one box,
+        # profiles/r03/driver_ab/; again in round 6, 0.1035-0.1055 -> 0.1109-0.1116,
+        # profiles/r06/driver/late_warmup.txt)
+        return ev, ev_grid, ev_first, n_iso
+
+    ISO_AFTER = os.environ.get("VR_BENCH_ISO_AFTER", "0") == "1"
+    if not ISO_AFTER:
+        ev, ev_grid, ev_first, n_iso = iso_phase()
 
     # N > 1: latency of ONE frame, first launch -> gathered and assembled on
     # rank 0, without the overlap of the pipelined loop
@@ -467,6 +475,8 @@ def main():
     dt = time.perf_counter() - t0
     dt = allreduce(dt, op=dist.ReduceOp.MAX)
     ms_per_step = dt / args.steps * 1e3
+    if ISO_AFTER:
+        ev, ev_grid, ev_first, n_iso = iso_phase()
     kern_ms = ev[0].elapsed_time(ev[1]) / n_iso
     kern_grid_ms = ev_grid[0].elapsed_time(ev_grid[1]) / n_iso
     kern_first_ms = ev_first[0].elapsed_time(ev_first[1]) / n_iso

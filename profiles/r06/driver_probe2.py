@@ -29,6 +29,8 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--reps", type=int, default=30)
 ap.add_argument("--config", default="C2")
 ap.add_argument("--spin", action="store_true")
+ap.add_argument("--prelude", action="store_true", help="also time runs that follow bench.py's isolated phase "
+                "(n launches one after the other on the current stream), interleaved with plain runs")
 ap.add_argument("--lean", action="store_true", help="also time a lean step: pre-built ctypes arguments, raw stream "
                 "handles, pre-made join events (no torch stream context, no per-step Event)")
 a = ap.parse_args()
@@ -125,6 +127,23 @@ def main():
             med = {k: round(statistics.median(r[k] for r in rs), 4) for k in rs[0]}
             print(json.dumps({"variant": name, "median": med, "host_ms_per_step": round(med["host_ms"] / a.steps, 5),
                               "host_minus_gpu_us": round((med["host_ms"] - med["gpu_ms"]) * 1e3, 1)}), flush=True)
+    if a.prelude:
+        def iso(n, schedule):
+            for _ in range(n):
+                vr.render_ex(scene, cfg.algorithm, cam, lit, info, W, H, pipe.bufs[0], band_rows=16, schedule=schedule)
+        variants = {"plain": lambda: None,
+                    "after_200_learned": lambda: iso(200, vr.Schedule.AUTO),
+                    "after_200_grid": lambda: iso(200, vr.Schedule.GRID),
+                    "after_200_first": lambda: [(vr.forget_orders(0), iso(1, vr.Schedule.AUTO)) for _ in range(200)]}
+        res = {k: [] for k in variants}
+        for _ in range(a.reps):
+            for k, f in variants.items():
+                f()
+                res[k].append(run(a.steps))
+        for k, rs in res.items():
+            med = {q: round(statistics.median(r[q] for r in rs), 4) for q in rs[0]}
+            print(json.dumps({"variant": k, "median": med, "host_ms_per_step": round(med["host_ms"] / a.steps, 5),
+                              "max_host_ms_per_step": round(max(r["host_ms"] for r in rs) / a.steps, 5)}), flush=True)
     steady = statistics.median(run(200)["gpu_ms"] / 200 for _ in range(5))
     rs = [run(a.steps) for _ in range(a.reps)]
     med = {k: round(statistics.median(r[k] for r in rs), 4) for k in rs[0]}

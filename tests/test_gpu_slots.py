@@ -171,3 +171,60 @@ def test_crawl_stats_credit_unloaded_reads(c5_scene):
     vr.render_ex(scene, vr.RayMarchAlgorithm.ORIGINAL, cam, lit, info, W, H, out, 0, 16, counter=ctr, stats=st)
     torch.cuda.synchronize()
     assert int(st[0]) == 0 and int(st[1]) == 0 and int(ctr.item()) > 0
+
+
+@pytest.mark.parametrize("algo", [vr.RayMarchAlgorithm.ORIGINAL, vr.RayMarchAlgorithm.LONGEST_AXIS],
+                         ids=lambda a: a.name)
+def test_prepared_render_in_the_frame_pipeline(c5_scene, algo):
+    """renderer.PreparedRender (the bench's per-frame host path): arguments made once, the
+    launch enqueued on the BandGather slot stream it is handed (no torch stream context).
+    Every frame of a pipelined run -- the crawl rows, with the moving-view rotation of three
+    prepared views -- equals render_ex's frame of the same view, and a camera changed in place
+    re-aims the next call."""
+    from voxelraymarcher_amd.tiles import BandGather
+    cfg, scene = c5_scene
+    W, H, r0, r1 = cfg.width, cfg.height, 688, 720
+    lit = vr.setup_constant_values()
+    info = vr.VoxelSceneInfo((0.0, 0.0, 0.0), cfg.scale)
+    cams = []
+    for k in (0, 1, 2):
+        c = vr.Camera.reference(W, H)
+        bits = np.array([c.raw.origin[0]], dtype=np.float32).view(np.uint32) + np.uint32(k)
+        c.raw.origin[0] = float(bits.view(np.float32)[0])
+        cams.append(c)
+    words = (r1 - r0) * W
+    refs = []
+    for c in cams:
+        ref = torch.full((words,), -1, dtype=torch.int32, device="cuda")
+        vr.render_ex(scene, algo, c, lit, info, W, H, ref, r0, r1)
+        refs.append(ref)
+    torch.cuda.synchronize()
+    preps = [vr.PreparedRender(scene, algo, c, lit, info, W, H, row_begin=r0, row_end=r1) for c in cams]
+    assert preps[0].vr_stream_arg
+    pipe = BandGather(W, r1 - r0, 16, 0, 1, torch.device("cuda", 0), depth=3)
+    pipe.bufs = [torch.full((words,), -1, dtype=torch.int32, device="cuda") for _ in range(3)]
+    got, k_box = [], [0]
+
+    def render(buf, stream=None):
+        preps[k_box[0] % 3](buf, stream)
+    render.vr_stream_arg = True
+    for k in range(24):
+        k_box[0] = k
+        pipe.step(render)
+        if len(pipe.pending) == pipe.depth:    # the oldest frame in flight: step k - 2's
+            slot = pipe.pending[0]
+            pipe.streams[slot].synchronize()
+            got.append((k - pipe.depth + 1, pipe.bufs[slot].clone()))
+            torch.cuda.current_stream().synchronize()   # (the copy is done before the slot renders again)
+    pipe.drain()
+    torch.cuda.synchronize()
+    bad = [k for k, f in got if not torch.equal(f, refs[k % 3])]
+    assert len(got) >= 20 and not bad, f"frames {bad[:5]} differ from render_ex's"
+    # the struct is passed by reference: moving camera 0 onto camera 1's eye gives camera 1's frame
+    cams[0].raw.origin[0] = cams[1].raw.origin[0]
+    out = torch.full((words,), -1, dtype=torch.int32, device="cuda")
+    preps[0](out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, refs[1])
+    with pytest.raises(ValueError):
+        preps[0](torch.empty(words - 1, dtype=torch.int32, device="cuda"))

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <mutex>
 #include <cerrno>
@@ -765,8 +766,32 @@ uint64_t crawl_key(uint64_t key, const vr::KView& v) {
     return key;
 }
 
+// VR_HOST_PROF (measurement builds only, profiles/build_variant.sh -- -DVR_HOST_PROF): host
+// clock stamps at the stages of each launch, fetched with vr_host_prof_fetch.
+#ifdef VR_HOST_PROF
+}  // namespace
+static uint64_t g_hp[4096][8];
+static uint32_t g_hp_n = 0;
+static inline uint64_t hp_now() { return (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count(); }
+extern "C" int vr_host_prof_fetch(uint64_t* out, int n) {
+    const uint32_t k = g_hp_n < 4096u ? g_hp_n : 4096u;
+    const uint32_t m = (uint32_t)n < k ? (uint32_t)n : k;
+    for (uint32_t i = 0; i < m; ++i)
+        for (int j = 0; j < 8; ++j) out[8 * i + j] = g_hp[(g_hp_n - m + i) % 4096u][j];
+    return (int)m;
+}
+namespace {
+#define VR_HP(i) hp_row[i] = hp_now()
+#else
+#define VR_HP(i) do { } while (0)
+#endif
 int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, uint32_t occupancy, vr::KView& v,
            void* stream) {
+#ifdef VR_HOST_PROF
+    uint64_t* hp_row = g_hp[g_hp_n++ % 4096u];
+    for (int j = 0; j < 8; ++j) hp_row[j] = 0;
+#endif
+    VR_HP(0);
     if (algo != VR_ALGO_ORIGINAL && algo != VR_ALGO_LONGESTAXIS) return fail(VR_E_INVALID, "unknown algorithm");
     if (kernel != VR_KERNEL_AUTO && kernel != VR_KERNEL_TILE && kernel != VR_KERNEL_TILE_REWALK)
         return fail(VR_E_INVALID, "unknown kernel (2, the persistent kernel, was retired)");
@@ -790,6 +815,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     SlotLease lease;
     int rc = lease.acquire(g_defer_ring, s->device, st);
     if (rc) return rc;
+    VR_HP(1);
     // An error after the slot was taken: the slot's event is recorded again on `st` first (a
     // stream-ordered free of its old buffers may already be queued there), then the error.
     auto bail = [&](hipError_t e, const char* what) {
@@ -811,6 +837,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     bool remake = false;
     // (the lock orders launches: "previous" is well defined)
     const bool alone = !D.any || D.last_stream == st || hipEventQuery(D.ev[D.last_idx]) == hipSuccess;
+    VR_HP(2);
     const bool heavy = schedule == VR_SCHEDULE_HEAVIEST_FIRST ||
                        (schedule == VR_SCHEDULE_AUTO && (alone || inflight_heavy()));
     // crawl records per wave: a lone frame ends with the crawl pass's longest chain (2 per
@@ -828,6 +855,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // renders as a first render does.
     const uint64_t key = view_key(s, algo, v);
     const bool repeat = D.last_key == key;
+    VR_HP(3);
     D.last_key = key;
     if (heavy && order_enabled() && n != 0) {
         if (n > O.cap) {
@@ -909,6 +937,7 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // deferred pixels stay 0): that needs a deferral that is not a function of the crawl key
     // below, which the kernels do not have (vr_internal.h KView, "end of the view's
     // identity"); tests/test_gpu_slots.py forces one (vr_debug_skip_next_crawl) to test the net.
+    VR_HP(4);
     bool crawl = true;
     {
         uint32_t lid = ++D.launch_serial;
@@ -937,13 +966,16 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     }
     // crawl pass grid from the records an earlier launch deferred (a hint: any grid renders
     // the same pixels)
+    VR_HP(5);
     const vr::KScene ks = kscene(s);
     const uint32_t cwgs = vr::crawl_grid(expect, v.crawl_rpw);
     // the tile pass's occupancy variant (vr_occupancy): AUTO = the in-flight one while another
     // stream's launch is running
     const bool hi = occupancy == VR_OCCUPANCY_IN_FLIGHT ||
                     (occupancy == VR_OCCUPANCY_AUTO && !alone && in_flight_occupancy());
+    VR_HP(6);
     hipError_t e = vr::launch_march((int)s->store, (int)algo, count, ks, v, st, cwgs, hi, crawl);
+    VR_HP(7);
     // The lane order first: when the slot has work-order buffers for this grid, perm_kernel
     // also writes the waves' costs under the new lane order and the work order is remade from
     // them at once -- an order made from costs walked under another lane order puts the light

@@ -319,6 +319,53 @@ def render_ex(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera, 
     return out
 
 
+class PreparedRender:
+    """One view's launch with its arguments made once (render_ex's options, without counter
+    or stats): calling it enqueues vr_render_ex into `out` on `stream` (a torch stream, or
+    None for the current one).  For a frame loop's per-frame host path: render_ex rebuilds
+    the options and re-checks the buffer on every call (~20 us of Python per frame, which a
+    20-frame timed loop pays up front while the GPU waits for its first frame;
+    profiles/r06/driver_probe2.py).  The camera and lighting structs are passed by reference,
+    so changing `camera.raw` in place re-aims the next call; out's size is checked once per
+    buffer.  `vr_stream_arg`: BandGather hands its slot stream over instead of entering a
+    torch stream context."""
+    vr_stream_arg = True
+
+    def __init__(self, scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera,
+                 lighting: _capi.VrLighting, info: VoxelSceneInfo, width: int, height: int, row_begin: int = 0,
+                 row_end: int | None = None, band_rows: int = 0, rank: int = 0, nranks: int = 1,
+                 kernel: Kernel = Kernel.AUTO, schedule: Schedule = Schedule.AUTO,
+                 occupancy: Occupancy = Occupancy.AUTO, tile_cols: int = 0, deal_stride: int = 0):
+        row_end = height if row_end is None else row_end
+        rows = row_end - row_begin
+        if tile_cols:
+            self.words = tile_buffer_words(width, rows, band_rows or max(1, rows), tile_cols, nranks)
+        else:
+            self.words = band_buffer_words(width, rows, band_rows or max(1, rows), nranks)
+        opts = _capi.VrRenderOpts()
+        check(lib().vr_render_opts_init(ctypes.byref(opts)), "vr_render_opts_init")
+        opts.kernel, opts.row_begin, opts.row_end = int(kernel), int(row_begin), int(row_end)
+        opts.band_rows, opts.rank, opts.nranks = int(band_rows), int(rank), int(nranks)
+        opts.schedule, opts.occupancy = int(schedule), int(occupancy)
+        opts.tile_cols, opts.deal_stride = int(tile_cols), int(deal_stride)
+        self._keep = (scene, camera, lighting, opts, f3(info.translation))   # (alive while prepared)
+        self._fn = lib().vr_render_ex
+        self._args = (scene.handle, int(algorithm), ctypes.byref(camera.raw), ctypes.byref(lighting),
+                      self._keep[4], int(info.scale), int(width), int(height), ctypes.byref(opts))
+        self._checked = set()
+
+    def __call__(self, out: torch.Tensor, stream=None) -> torch.Tensor:
+        key = (out.data_ptr(), out.numel(), out.dtype, out.is_contiguous())
+        if key not in self._checked:
+            _require_u32(out, self.words)
+            self._checked.add(key)
+        sh = (stream if stream is not None else torch.cuda.current_stream()).cuda_stream
+        rc = self._fn(*self._args, c_void_p(key[0]), c_void_p(sh))
+        if rc:
+            check(rc, "vr_render_ex")
+        return out
+
+
 def run_raymarching_kernel(scene: DeviceScene, algorithm: RayMarchAlgorithm, camera: Camera,
                            lighting: _capi.VrLighting, info: VoxelSceneInfo, width: int, height: int,
                            out: torch.Tensor | None = None, row_begin: int = 0, row_end: int | None = None,

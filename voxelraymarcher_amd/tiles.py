@@ -300,6 +300,7 @@ class BandGather:
         # copy has finished.
         self.side = torch.cuda.Stream(dev) if (cuda and rank == 0 and x) else None
         self.copied = [None] * depth
+        self.joins = [None] * depth  # per slot: the event its stream waits on for the caller's work
         self.pending = []            # slots in submission order
         self.on_frame = on_frame     # rank 0: callback(frame[:H]) after each assembled frame
         self.k = 0
@@ -390,13 +391,26 @@ class BandGather:
         self.pending.remove(slot)
 
     def step(self, render) -> None:
-        """render(buf) enqueues this rank's bands on the current stream."""
+        """render(buf) enqueues this rank's bands on the current stream (or, with a
+        `vr_stream_arg` attribute and no exchange, render(buf, stream) on the given one)."""
         slot = self.k % self.depth
         if slot in self.pending:
             self._finish(slot)
-        if self.streams is not None:
-            # the slot's stream picks up after the caller's work (inputs, earlier frames' users)
-            self.streams[slot].wait_stream(torch.cuda.current_stream()) if self.k < self.depth else None
+        if self.streams is not None and self.k < self.depth:
+            # the slot's stream picks up after the caller's work (inputs, earlier frames' users);
+            # one made event per slot, recorded again each time (wait_stream makes a new one)
+            if self.joins[slot] is None:
+                self.joins[slot] = torch.cuda.Event()
+            self.joins[slot].record(torch.cuda.current_stream())
+            self.streams[slot].wait_event(self.joins[slot])
+        if not self.x and self.streams is not None and getattr(render, "vr_stream_arg", False):
+            # a render that takes the stream (renderer.PreparedRender): no torch stream context,
+            # the host path of a frame is one ctypes call
+            render(self.bufs[slot], self.streams[slot])
+            self.pending.append(slot)
+            self.last = slot
+            self.k += 1
+            return
         with self._slot_stream(slot):
             render(self.bufs[slot])
             if self.x:
