@@ -239,8 +239,9 @@ typedef struct {
 typedef enum {
     VR_OCCUPANCY_AUTO = 0,
     VR_OCCUPANCY_LONE = 1,        /* the lone-frame variant (7 waves/SIMD original, 6 longest axis) */
-    VR_OCCUPANCY_IN_FLIGHT = 2    /* the frames-in-flight variant where one exists (cuckoo original 8,
-                                     VCS longest axis 7) */
+    VR_OCCUPANCY_IN_FLIGHT = 2    /* the frames-in-flight variant where one exists (a build knob:
+                                     since round 6 every walk runs its lone kernel in flight too,
+                                     VR_ORIG_WAVES_HI / VR_LONG_WAVES_HI in vr_march.hip) */
 } vr_occupancy;
 
 /* Defaults: struct_size = sizeof(vr_render_opts), kernel AUTO, rows [0, UINT32_MAX) --

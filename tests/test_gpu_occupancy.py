@@ -1,12 +1,13 @@
 """The tile pass's occupancy variants, forced (vr_render_opts.occupancy, include/vr.h).
 
-With frames in flight the AUTO schedule renders the cuckoo `original` walk at 8 waves per
-SIMD and the VCS `longestaxis` walk at 7 (vr_march.hip TileWaves, march_kernel<..., true>)
--- the kernels C3's and C4's pipelined bench loops run -- but AUTO picks them only when
-another stream's launch is still running, which a test cannot arrange deterministically.
-VR_OCCUPANCY_IN_FLIGHT forces them: every frame here is rendered by the in-flight variant
-and must equal the committed oracle digest (tests/golden/frames.json) and the lone
-variant's frame, pixel for pixel.
+With frames in flight the AUTO schedule renders with the in-flight occupancy variant of a walk
+where a build has one (vr_march.hip TileWaves, march_kernel<..., true>: rounds 4-5 ran the
+cuckoo `original` walk at 8 waves per SIMD and the VCS `longestaxis` walk at 7; since round 6
+every walk is fastest in flight with its lone kernel, so the default build launches that), but
+AUTO picks it only when another stream's launch is still running, which a test cannot arrange
+deterministically.  VR_OCCUPANCY_IN_FLIGHT forces it: every frame here is rendered through the
+in-flight path and must equal the committed oracle digest (tests/golden/frames.json) and the
+lone variant's frame, pixel for pixel.
   C4: CuckooHashTable::lookupVoxel (CuckooHashTable.cuh:59-76) in rayMarchVoxelGrid
       (Renderer.cuh:260-336), the whole 1920x1080 frame over the 20 M-voxel store;
   C3: rayMarchVoxelGridLongestAxis / performVoxelSpaceJump (Renderer.cuh:696-915), the
@@ -14,7 +15,7 @@ variant's frame, pixel for pixel.
   C5 longest axis: the whole 3840x2160 frame (its crawl rows walk up to 1.4 million
       iterations, deferred to the crawl pass) and the committed longest walks
       (tests/golden/c5_crawl_pixels.json).
-The VCS `original` walk has no in-flight variant (8 waves measured slower); forcing it
+The VCS `original` walk never had an in-flight variant (8 waves measured slower); forcing it
 renders with the lone kernel, which is checked too."""
 from __future__ import annotations
 
@@ -65,7 +66,7 @@ def test_in_flight_variant_full_frame(name, cfg_name, algo):
 
 
 def test_in_flight_variant_c5_longest_axis():
-    """C5, longest axis, forced in-flight variant (7 waves/SIMD): the whole 4K frame
+    """C5, longest axis, forced in-flight variant (the lone kernel unless a build makes one): the whole 4K frame
     against the committed digest, and the committed longest walks (rows 696-711)."""
     cfg = vr.CONFIGS["C5"]
     scene = vr.create_scene(*cfg.voxels(), vr.StorageType.VOXEL_CLUSTER_STORE)

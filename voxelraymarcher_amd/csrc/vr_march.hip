@@ -1318,7 +1318,13 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
         if (SHADOW) {
             // the light: its axis order, longest-axis direction and sign classes are
             // made on the host (kernel arguments: SGPRs), one pass
-            const f3 ds = ld3(v.Lw);
+            f3 ds = ld3(v.Lw);
+            // (held in VGPRs, though uniform: as SGPRs the direction and everything made from
+            // it -- sign classes, plane offsets, the divisions' operands -- overflowed the
+            // SGPR file, and the shadow loops restored spilled SGPRs with 16-22 v_readlane per
+            // iteration; as VGPRs, 2-6: C3 per frame in flight 0.1888 -> 0.1863 ms, first
+            // render 0.2815 -> 0.2758, profiles/r06/ab/ab_C3_vdir.txt)
+            asm volatile("" : "+v"(ds.x), "+v"(ds.y), "+v"(ds.z));
             if (v.L_unit) {
                 hit = walk_longest_vcs<SHADOW, true, 2, 1, 0>(oo, ds, v.L_cls, reg, tail, hcol, hcode);
             } else {
@@ -1710,9 +1716,16 @@ __device__ __forceinline__ void add_ff(const KView& v, uint32_t lane, unsigned l
 #ifndef VR_ORIG_WAVES_HI
 #define VR_ORIG_WAVES_HI 7
 #endif
+// (Round 6: 6 for the VCS longest-axis walk too, the lone kernel's, so frames in flight run
+// that kernel.  With its shadow direction in VGPRs and the direction made per region round
+// the 7-wave variant spills 30 VGPRs and 212 SGPRs: C3 per frame in flight 0.1851 -> 0.1835 ms
+// at 6, profiles/r06/ab/ab_C3_waves_hi.txt.)
 #ifndef VR_LONG_WAVES_HI
-#define VR_LONG_WAVES_HI 7
+#define VR_LONG_WAVES_HI 6
 #endif
+// (a variant equal to the lone one is not built: both launch the lone kernel)
+constexpr bool kLongHiVariant = VR_LONG_WAVES_HI != VR_LONG_WAVES;
+constexpr bool kOrigHiVariant = VR_ORIG_WAVES_HI != VR_ORIG_WAVES;
 template <int ALGO, bool HI> struct TileWaves {
     static constexpr int value = ALGO == ALGO_ORIGINAL ? (HI ? VR_ORIG_WAVES_HI : VR_ORIG_WAVES)
                                                        : (HI ? VR_LONG_WAVES_HI : VR_LONG_WAVES);
@@ -2135,11 +2148,11 @@ hipError_t launch_march(int store, int algo, bool count, const KScene& s, const 
     const bool hi = in_flight && !count;
     if (store == STORE_VCS) {
         if (algo == ALGO_ORIGINAL) { if (count) VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, true); else VR_LAUNCH(STORE_VCS, ALGO_ORIGINAL, false); }
-        else if (hi) VR_LAUNCH_HI(STORE_VCS, ALGO_LONGEST, false, true);
+        else if (hi && kLongHiVariant) VR_LAUNCH_HI(STORE_VCS, ALGO_LONGEST, false, true);
         else { if (count) VR_LAUNCH(STORE_VCS, ALGO_LONGEST, true); else VR_LAUNCH(STORE_VCS, ALGO_LONGEST, false); }
     } else {
         if (algo == ALGO_ORIGINAL) {
-            if (hi) VR_LAUNCH_HI(STORE_HASH, ALGO_ORIGINAL, false, true);
+            if (hi && kOrigHiVariant) VR_LAUNCH_HI(STORE_HASH, ALGO_ORIGINAL, false, true);
             else if (count) VR_LAUNCH(STORE_HASH, ALGO_ORIGINAL, true);
             else VR_LAUNCH(STORE_HASH, ALGO_ORIGINAL, false);
         }

@@ -273,7 +273,9 @@ class Schedule(enum.IntEnum):
 
 class Occupancy(enum.IntEnum):
     """vr_occupancy: the tile pass's occupancy variant (identical pixels).  AUTO: the in-flight
-    variant (cuckoo original 8 waves/SIMD, VCS longest axis 7) while another stream's launch runs."""
+    variant while another stream's launch runs -- where one is built (vr_march.hip
+    VR_ORIG_WAVES_HI / VR_LONG_WAVES_HI; round 6 measured every walk fastest in flight with its
+    lone kernel, so by default IN_FLIGHT launches that kernel)."""
     AUTO = _capi.VR_OCCUPANCY_AUTO
     LONE = _capi.VR_OCCUPANCY_LONE
     IN_FLIGHT = _capi.VR_OCCUPANCY_IN_FLIGHT
