@@ -789,34 +789,38 @@ struct Walker : Ctx<STORE, COUNT, ExactWalk<STORE, CRAWL>::value ? kCrawlBudget 
             const uint32_t* freg = s.ht_filter + (size_t)reg * kHashFilterWords;
             uint32_t fw = 0, bit = 0;
             uint32_t ic = this->iters + (0x42800000u - kBudget);   // biased count (see the VCS walk)
+            // rayMarchVoxelGrid's voxel step (Renderer.cuh:318-331) from o: its t values, min
+            auto voxel_step = [&](float& sX, float& sY, float& sZ) -> float {
+                const float ax = next_plane_fma(o.x, gx, ex) - o.x, ay = next_plane_fma(o.y, gy, ey) - o.y,
+                            az = next_plane_fma(o.z, gz, ez) - o.z;
+                if (EQ) {                                 // see grid_original
+                    const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
+                    float sMin = div_fast(am, rx);
+                    if (!okw) {
+                        const bool bad = !(am >= nlim);
+                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) sMin = bad ? am / fabsf(d.x) : sMin;
+                    }
+                    return sMin;
+                }
+                sX = div_fast(ax, rx); sY = div_fast(ay, ry); sZ = div_fast(az, rz);
+                if (!okw) {
+                    const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
+                    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+                        sX = bad ? (zx ? kInf : ax / d.x) : sX;
+                        sY = bad ? (zy ? kInf : ay / d.y) : sY;
+                        sZ = bad ? (zz ? kInf : az / d.z) : sZ;
+                    }
+                }
+                return fminf(sX, fminf(sY, sZ));
+            };
             for (;;) {
                 const int32_t vx = f2i(o.x), vy = f2i(o.y), vz = f2i(o.z);
                 const uint32_t wi = this->word_index((uint32_t)vx, (uint32_t)vy, (uint32_t)vz);
                 fw = freg[wi];
                 __builtin_amdgcn_sched_barrier(0);   // issue the load before the step
-                // rayMarchVoxelGrid's voxel step (Renderer.cuh:318-331), while the word loads
-                const float ax = next_plane_fma(o.x, gx, ex) - o.x, ay = next_plane_fma(o.y, gy, ey) - o.y,
-                            az = next_plane_fma(o.z, gz, ez) - o.z;
-                float sMin, sX = 0.0f, sY = 0.0f, sZ = 0.0f;
-                if (EQ) {                                 // see grid_original
-                    const float am = fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az)));
-                    sMin = div_fast(am, rx);
-                    if (!okw) {
-                        const bool bad = !(am >= nlim);
-                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) sMin = bad ? am / fabsf(d.x) : sMin;
-                    }
-                } else {
-                    sX = div_fast(ax, rx); sY = div_fast(ay, ry); sZ = div_fast(az, rz);
-                    if (!okw) {
-                        const bool bad = !(fminf(fabsf(ax), fminf(fabsf(ay), fabsf(az))) >= nlim);
-                        if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
-                            sX = bad ? (zx ? kInf : ax / d.x) : sX;
-                            sY = bad ? (zy ? kInf : ay / d.y) : sY;
-                            sZ = bad ? (zz ? kInf : az / d.z) : sZ;
-                        }
-                    }
-                    sMin = fminf(sX, fminf(sY, sZ));
-                }
+                // the voxel step while the word loads
+                float sX = 0.0f, sY = 0.0f, sZ = 0.0f;
+                const float sMin = voxel_step(sX, sY, sZ);
                 // key1 + key2 of a key the tables do not hold; the hit's own bytes are
                 // settled after the loop (8 or 12)
                 this->count(8u);
