@@ -37,6 +37,9 @@ p.add_argument("--layout", default="tiles", choices=["tiles", "bands", "strips"]
 p.add_argument("--strip-iters", type=int, default=12, help="strips: rebalancing rounds")
 p.add_argument("--strip-steps", type=int, default=80, help="strips: pipelined frames timed per rank per round")
 p.add_argument("--strip-align", type=int, default=4)
+p.add_argument("--latency-cut", action="store_true",
+               help="strips: also learn a second cut from the ranks' LONE-frame times (grid order, a first "
+                    "render: the single frame of the reference's CLI) and project one frame's latency with it")
 p.add_argument("--tile-cols", type=int, default=16)
 p.add_argument("--latency-reps", type=int, default=30)
 p.add_argument("--tiling", default="fixed", choices=["fixed", "weak"],
@@ -169,6 +172,26 @@ for r in ([int(x) for x in a.ranks.split(",")] if a.ranks else range(a.world)):
     ranks.append({"rank": r, "ms_per_frame": round(ms, 4),
                   "lone_frame_ms_grid": round(lg, 4), "lone_frame_ms_learned": round(ll, 4)})
     print(json.dumps(ranks[-1]), flush=True)
+latency_cut = None
+if STRIPS and a.latency_cut:
+    # the latency-balanced strips: the same rebalancing, from each rank's lone frame time
+    thr_bounds, cal_l, est = bounds, [], None
+    bounds = strip_bounds([1.0] * H, a.world, a.strip_align)
+    for it in range(a.strip_iters):
+        ts = [lone(r, a.world, vr.Schedule.GRID) for r in range(a.world)]
+        cal_l.append({"bounds": list(bounds), "lone_ms_grid": [round(t, 4) for t in ts]})
+        print(json.dumps({"latency_round": it, **cal_l[-1]}), flush=True)
+        bounds, est = rebalance_strips(bounds, ts, a.strip_align, prior=est)
+    bounds = min(cal_l, key=lambda c: max(c["lone_ms_grid"]))["bounds"]
+    lg = [lone(r, a.world, vr.Schedule.GRID) for r in range(a.world)]
+    ll = [lone(r, a.world, vr.Schedule.HEAVIEST_FIRST) for r in range(a.world)]
+    latency_cut = {"bounds": bounds, "calibration": cal_l,
+                   "lone_frame_ms_grid": [round(x, 4) for x in lg], "lone_frame_ms_learned": [round(x, 4) for x in ll],
+                   "projected_lone_frame_ms": {"grid": round(max(lg), 4), "learned": round(max(ll), 4)},
+                   "projected_latency_speedup": {"grid": round(single_lone["grid"] / max(lg), 2),
+                                                 "learned": round(single_lone["learned"] / max(ll), 2)}}
+    print(json.dumps({"latency_cut": latency_cut}), flush=True)
+    bounds = thr_bounds
 slow = max(x["ms_per_frame"] for x in ranks)
 slow_lg = max(x["lone_frame_ms_grid"] for x in ranks)
 slow_ll = max(x["lone_frame_ms_learned"] for x in ranks)
@@ -185,5 +208,6 @@ print(json.dumps({"config": a.config, "width": W, "height": H, "world": a.world,
                   "projected_lone_frame_ms": {"grid": slow_lg, "learned": slow_ll},
                   "projected_latency_speedup": {"grid": round(single_lone["grid"] / slow_lg, 2),
                                                 "learned": round(single_lone["learned"] / slow_ll, 2)},
+                  "latency_cut": latency_cut,
                   "note": "max over ranks of each rank's own pipelined frame time on one GPU; RCCL gather not "
                           "included (overlapped with the next frame in bench.py)"}), flush=True)
