@@ -360,6 +360,8 @@ class PreparedRender:
         key = (out.data_ptr(), out.numel(), out.dtype, out.is_contiguous())
         if key not in self._checked:
             _require_u32(out, self.words)
+            if len(self._checked) >= 64:          # (a loop over many buffers: keep the set small)
+                self._checked.clear()
             self._checked.add(key)
         sh = (stream if stream is not None else torch.cuda.current_stream()).cuda_stream
         rc = self._fn(*self._args, c_void_p(key[0]), c_void_p(sh))
