@@ -145,6 +145,8 @@ HEADLINE = "Mrays/sec at 1920x1080, 256^3 grid (VCS+original); achieved HBM GB/s
 # (C5 8-rank projection 6.48x with 12 rounds on 4-row steps, 6.40x with 8 on 8-row steps;
 # profiles/r06/strips/)
 STRIP_ITERS, STRIP_WARM, STRIP_STEPS, STRIP_ALIGN = 12, 16, 80, 4
+# the latency cut's lone frames per rank and round (after LAT_WARM untimed ones)
+LAT_WARM, LAT_REPS = 4, 7
 
 
 def learn_strips(pipe, render_rows, W, H, world, rank, dev, stage_host, grouped) -> list:
@@ -183,6 +185,38 @@ def learn_strips(pipe, render_rows, W, H, world, rank, dev, stage_host, grouped)
     # the measured cut whose slowest rank is fastest (the cost model -- uniform within a strip --
     # is coarse where a few rows cost most, C5's crawl rows: its last re-cut is not always the best)
     best = min(hist, key=lambda h: max(h["ms_per_frame"]))
+    pipe.set_strips(best["strips"])
+    return hist
+
+
+def learn_latency_strips(pipe, render_rows, W, H, world, rank, dev, stage_host, grouped) -> list:
+    """The latency-balanced cut (profiles/rank_projection.py --latency-cut): as learn_strips, but
+    each rank times ONE frame of its strip alone (HIP events around the launch on the current
+    stream, median of LAT_REPS after LAT_WARM), so the ranks' single-frame latencies are equal --
+    the crawl rows' rank gets a short strip.  Returns the rounds; pipe is left with the best cut."""
+    from voxelraymarcher_amd.tiles import rebalance_strips
+    bounds, est, hist = list(pipe.S), None, []
+    buf = torch.empty(W * H, dtype=torch.int32, device=dev)
+    cur = torch.cuda.current_stream()
+    for _ in range(STRIP_ITERS):
+        y0, y1 = bounds[rank], bounds[rank + 1]
+        ts = []
+        for k in range(LAT_WARM + LAT_REPS):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cur)
+            render_rows(buf, y0, y1)
+            e1.record(cur)
+            torch.cuda.synchronize()
+            if k >= LAT_WARM:
+                ts.append(e0.elapsed_time(e1))
+        t = torch.zeros(world, dtype=torch.float64, device="cpu" if stage_host else dev)
+        t[rank] = float(np.median(ts))
+        if grouped:
+            dist.all_reduce(t)
+        tv = [float(x) for x in t.cpu().tolist()]
+        hist.append({"strips": list(bounds), "lone_ms": [round(x, 4) for x in tv]})
+        bounds, est = rebalance_strips(bounds, tv, STRIP_ALIGN, prior=est)
+    best = min(hist, key=lambda h: max(h["lone_ms"]))
     pipe.set_strips(best["strips"])
     return hist
 
@@ -495,6 +529,33 @@ def main():
     dt_mov = allreduce(time.perf_counter() - t1, op=dist.ReduceOp.MAX)
     ms_moving = dt_mov / args.steps * 1e3
 
+    # N > 1 with learned strips: a second cut, balanced on one frame's latency instead of the
+    # pipelined rate, and the latency of one frame on it (after the timed loops: the strips and
+    # the learned orders of their views change)
+    frame_latency_cut_ms, lat_hist = None, []
+    thr_strips = list(pipe.S) if strip else None
+    if strip and grouped:
+        lat_hist = learn_latency_strips(pipe, lambda buf, y0, y1: vr.render_ex(scene, cfg.algorithm, cam, lit, info,
+                                                                               W, H, buf, y0, y1),
+                                        W, H, world, rank, dev, stage_host, grouped)
+        render_lat = prepare(cam)
+        for _ in range(16):                     # the new strip's orders learned
+            pipe.step(render_lat)
+        pipe.drain()
+        lat = []
+        for _ in range(5):
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pipe.step(render_lat)
+            pipe.drain()
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t0)
+        frame_latency_cut_ms = allreduce(float(np.median(lat)) * 1e3, op=dist.ReduceOp.MAX)
+        if args.dump_frame and rank == 0:           # (the last frame on the latency cut, for the tests)
+            root, ext = os.path.splitext(args.dump_frame)
+            np.save(root + ".latency_cut" + (ext or ".npy"), pipe.last_frame().cpu().numpy())
+
     if rank == 0:
         def gbs(nbytes, ms):
             return nbytes / (ms * 1e-3) / 1e9
@@ -647,15 +708,24 @@ def main():
             "dispatch_phases": {"strip_calibration": STRIP_ITERS * (STRIP_WARM + STRIP_STEPS) if strip else 0,
                                 "warmup": args.warmup, "iso_first": n_iso, "untimed": 40, "iso_grid": n_iso,
                                 "iso_learned": n_iso,
-                                "latency": 5 if grouped else 0, "timed": args.steps, "moving": args.steps},
+                                "latency": 5 if grouped else 0, "timed": args.steps, "moving": args.steps,
+                                "latency_cut": (STRIP_ITERS * (LAT_WARM + LAT_REPS) + 16 + 5) if lat_hist else 0},
         }
         if strip:
-            line["config"]["strip_bounds"] = pipe.S
+            line["config"]["strip_bounds"] = thr_strips
             line["config"]["strip_calibration"] = strip_hist
+            if lat_hist:
+                line["config"]["latency_strip_bounds"] = pipe.S
+                line["config"]["latency_calibration"] = lat_hist
         if HW_QUEUES_REQUESTED is not None:
             line["config"]["hw_queues_requested"] = HW_QUEUES_REQUESTED
         if frame_latency_ms is not None:
             line["frame_latency_ms"] = round(frame_latency_ms, 4)
+        if frame_latency_cut_ms is not None:
+            line["frame_latency_ms_latency_cut"] = round(frame_latency_cut_ms, 4)
+            line["frame_latency_basis"] = ("frame_latency_ms: one frame first launch -> gathered on rank 0 on the "
+                                           "throughput cut (config.strip_bounds); _latency_cut: the same on strips "
+                                           "re-cut from the ranks' lone-frame times (config.latency_strip_bounds)")
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, xyz, rgb, args.cpu_threads or baseline_threads())
         print(json.dumps(line), flush=True)

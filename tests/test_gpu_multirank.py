@@ -102,6 +102,13 @@ def test_bench_frame_path_ranks_share_one_gpu(world, layout, tmp_path):
         b = line["config"]["strip_bounds"]
         assert len(b) == world + 1 and b[0] == 0 and b[-1] == H and all(b[i] < b[i + 1] for i in range(world))
         assert len(line["config"]["strip_calibration"]) >= 1
+        # the second, latency-balanced cut (round 6): its own strips, its one-frame latency, and
+        # its last assembled frame equal to the oracle's too
+        lb = line["config"]["latency_strip_bounds"]
+        assert len(lb) == world + 1 and lb[0] == 0 and lb[-1] == H and all(lb[i] < lb[i + 1] for i in range(world))
+        assert line["frame_latency_ms_latency_cut"] > 0 and len(line["config"]["latency_calibration"]) >= 1
+        got_l = np.load(str(dump).replace(".npy", ".latency_cut.npy"))
+        assert np.array_equal(got_l, _oracle_rgb8("C2", W, H)), "latency-cut frame differs from the oracle"
     # the frame's algorithmic bytes are the sum over the ranks' bands (all-reduced)
     assert line["roofline"]["algorithmic_bytes_per_frame"] > line["roofline"]["algorithmic_bytes_per_launch"]
     got = np.load(dump)
