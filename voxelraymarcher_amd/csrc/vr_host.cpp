@@ -692,6 +692,17 @@ uint32_t crawl_rpw_override() {
     }();
     return r;
 }
+// VR_CRAWL_RPW_IN_FLIGHT (A/B runs): crawl records per wave with frames in flight (default 32:
+// fewer crawl waves leave the CU slots to the other frames' tile passes; C5 per frame in flight
+// 0.5611-0.5659 ms at 8, 0.5409-0.5647 at 32, never slower; profiles/r06/ab/ab_C5_crawl_rpw.txt).
+uint32_t crawl_rpw_in_flight() {
+    static const uint32_t r = [] {
+        const char* e = std::getenv("VR_CRAWL_RPW_IN_FLIGHT");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (uint32_t)(v >= 1 && v <= 64 ? v : 32);
+    }();
+    return r;
+}
 // VR_INFLIGHT_WAVES=0 (A/B runs): frames in flight keep the lone-frame occupancy.
 bool in_flight_occupancy() {
     static const bool on = [] {
@@ -843,8 +854,8 @@ int launch(const vr_scene* s, vr_algo algo, uint32_t kernel, uint32_t schedule, 
     // crawl records per wave: a lone frame ends with the crawl pass's longest chain (2 per
     // wave since round 4's shorter chains: C5 alone 0.767 -> 0.759 ms vs 4,
     // profiles/r04/crawl/scene_lds_ab.txt, rpw_multi_cluster.txt); with frames in flight the
-    // pass's issue cycles are what count (8 per wave)
-    v.crawl_rpw = crawl_rpw_override() ? crawl_rpw_override() : (alone ? 2u : 8u);
+    // pass's issue cycles are what count (32 per wave since round 6; crawl_rpw_in_flight)
+    v.crawl_rpw = crawl_rpw_override() ? crawl_rpw_override() : (alone ? 2u : crawl_rpw_in_flight());
     D.any = true;
     D.last_stream = st;
     D.last_idx = lease.idx;

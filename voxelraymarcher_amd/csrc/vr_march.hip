@@ -1900,7 +1900,10 @@ __global__ __launch_bounds__(1024) void order_kernel(const uint32_t* __restrict_
 #define VR_CRAWL_RPW 4
 #endif
 constexpr uint32_t kCrawlRpw = VR_CRAWL_RPW;
-constexpr uint32_t kCrawlMaxRpw = 16;     // records per wave with an LDS bitmap slot
+#ifndef VR_CRAWL_MAX_RPW
+#define VR_CRAWL_MAX_RPW 32
+#endif
+constexpr uint32_t kCrawlMaxRpw = VR_CRAWL_MAX_RPW;     // records per wave with an LDS bitmap slot
 // Workgroup shape: 2 waves (as the tile pass).  (Round 4 measured an opt-in mode that cached
 // the scene's whole region table and cluster bits in each 8-wave workgroup's LDS: no faster
 // alone, slower in flight, profiles/r04/crawl/scene_lds_ab.txt -- removed in round 5.)
@@ -1932,7 +1935,8 @@ __global__ __launch_bounds__(64 * kCrawlWaves) void crawl_kernel(KScene s, KView
     // the walk, so fewer lanes per wave -- spread over more waves -- finish sooner
     // (v.crawl_rpw: the host's choice per launch -- 4 for a lone frame, whose time is the
     // longest record's chain; 8 with frames in flight, where the pass's issue cycles count:
-    // C5 0.6707 -> 0.6514 ms per frame, profiles/r03/rpw_deep/)
+    // C5 0.6707 -> 0.6514 ms per frame, profiles/r03/rpw_deep/; 32 since round 6, which leaves
+    // more CU slots to the other frames' tile passes: 0.563 -> 0.542, ab_C5_crawl_rpw.txt)
     const uint32_t rpw = v.crawl_rpw ? v.crawl_rpw : kCrawlRpw;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, wlane = threadIdx.x & 63u;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
