@@ -1935,8 +1935,8 @@ __global__ __launch_bounds__(64 * kCrawlWaves) void crawl_kernel(KScene s, KView
     // the walk, so fewer lanes per wave -- spread over more waves -- finish sooner
     // (v.crawl_rpw: the host's choice per launch -- 4 for a lone frame, whose time is the
     // longest record's chain; 8 with frames in flight, where the pass's issue cycles count:
-    // C5 0.6707 -> 0.6514 ms per frame, profiles/r03/rpw_deep/; 32 since round 6, which leaves
-    // more CU slots to the other frames' tile passes: 0.563 -> 0.542, ab_C5_crawl_rpw.txt)
+    // C5 0.6707 -> 0.6514 ms per frame, profiles/r03/rpw_deep/; 32 since round 6, never slower
+    // and in some runs 4 % faster, vr_host.cpp crawl_rpw_in_flight)
     const uint32_t rpw = v.crawl_rpw ? v.crawl_rpw : kCrawlRpw;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, wlane = threadIdx.x & 63u;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
