@@ -695,7 +695,7 @@ uint32_t crawl_rpw_override() {
 // VR_CRAWL_RPW_IN_FLIGHT (A/B runs): crawl records per wave with frames in flight (default 32:
 // fewer crawl waves for the other frames' tile passes to share the CUs with.  C5 per frame in
 // flight is bimodal from run to run -- 0.541-0.543 ms in some processes, 0.561-0.567 in others --
-// and the fast mode showed up in 6 of 16 runs at 32 or 64 and in none of 14 at 8; never slower;
+// and the fast mode showed up in 6 of 20 runs at 32 or more and in none of 22 at 8 or 16; never slower;
 // profiles/r06/ab/ab_C5_crawl_rpw.txt).
 uint32_t crawl_rpw_in_flight() {
     static const uint32_t r = [] {
